@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark: EDS+DAH squares/s on MI355X (BASELINE.json metric).
+
+One step = the whole hot path (ODS -> EDS -> 4k NMT roots -> data root) over
+one batch of `--batch` random-namespace k x k squares per rank, inputs already
+resident in HBM (cda_extend_dah_device).  Ranks shard independent squares (no
+collective on the data path: SURVEY.md 8(e), config 4) -> "scaling": "weak".
+Timing: W untimed steps, then K steps bracketed by barrier + synchronize, max
+over ranks.  Rank 0 prints one JSON line.
+
+Extra fields: per-stage HIP-event times and rooflines, single-square latency
+(k=128, config 2), k=512 single square (config 3, GF(2^16)), and the CPU
+baseline (oracle/cda_oracle.c "port", same rsmt2d structure, host threads).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "celestia-app_amd"))
+
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s spec
+PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s
+SHA_OPS = 1384                 # int32 VALU ops per SHA-256 compression on gfx950
+SHARE = 512
+
+
+def compressions(k: int) -> dict:
+    W = 2 * k
+    return {
+        "nmt_leaves": 9 * W * W,                 # 542-B leaf message = 9 blocks, one per EDS cell
+        "nmt_levels": 3 * 2 * W * (W - 1),      # 181-B node message = 3 blocks
+        "data_root": 2 * 2 * W + 2 * (2 * W - 1),
+    }
+
+
+def rs_bytes(k: int) -> int:
+    return 4 * k * k * SHARE                     # ODS read + 3 parity quadrants written
+
+
+def stage_report(st: dict, k: int, batch: int) -> dict:
+    out = {}
+    comp = compressions(k)
+    for name, (ms, n) in st.items():
+        if n == 0:
+            continue
+        avg = ms / n
+        rec = {"avg_ms": avg, "launches": n}
+        if name in comp:
+            ops = comp[name] * batch * SHA_OPS
+            rec.update(bound="valu", achieved=ops / (avg * 1e-3) / 1e12, peak=PEAK_VALU_TOPS, unit="Tops/s")
+        elif name in ("rs_q0", "rs_q3"):
+            # rs_q0: read ODS, write Q0|Q1|Q2 (4 k^2 shares); rs_q3: read Q2, write Q3 (2 k^2 shares)
+            byt = (4 if name == "rs_q0" else 2) * k * k * SHARE * batch
+            rec.update(bound="hbm", achieved=byt / (avg * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
+        if "achieved" in rec:
+            rec["frac"] = rec["achieved"] / rec["peak"]
+        out[name] = rec
+    return out
+
+
+def load_traffic(stage: str):
+    """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary
+    (profiles/pmc_*.json, written by tools/pmc_summary.py), else None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+        return d.get(stage, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(k: int, seconds: float, threads: int):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle
+    ods = coracle.random_square(k, 0)
+    coracle.cpu_baseline(ods, threads)          # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        coracle.cpu_baseline(ods, threads)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 1000:
+            break
+    return {"value": n / el, "unit": "squares/s", "cores": threads, "kind": "port",
+            "sample": f"{n} squares k={k} (C restatement, rsmt2d structure: each cell hashed per axis, "
+                      f"{threads} host threads, {el:.1f}s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=128, help="squares per rank per step")
+    ap.add_argument("--distinct", type=int, default=8, help="distinct input squares per rank (tiled)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip k=512 and latency extras")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from celestia_da import Context, testfactory
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    k, B = args.k, args.batch
+    W = 2 * k
+    ctx = Context(local)
+
+    # inputs: distinct random squares per rank, tiled to the batch
+    nd = max(1, min(args.distinct, B))
+    base = np.stack([testfactory.random_square(k, rank * 100000 + i) for i in range(nd)])
+    ods_h = np.concatenate([base] * ((B + nd - 1) // nd))[:B]
+    d_ods = torch.from_numpy(np.ascontiguousarray(ods_h)).to(dev)
+    d_eds = torch.empty(B * W * W * SHARE, dtype=torch.uint8, device=dev)
+    d_rows = torch.empty(B * W * 90, dtype=torch.uint8, device=dev)
+    d_cols = torch.empty(B * W * 90, dtype=torch.uint8, device=dev)
+    d_roots = torch.empty(B * 32, dtype=torch.uint8, device=dev)
+    d_status = torch.empty(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        ctx.extend_dah_device(d_ods.data_ptr(), k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
+                              d_roots.data_ptr(), d_status.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    assert int(d_status.abs().sum().item()) == 0, "push-order status set on ordered input"
+    # tiled inputs must give tiled data roots
+    roots = d_roots.view(B, 32).cpu().numpy()
+    for i in range(nd, B):
+        assert (roots[i] == roots[i % nd]).all()
+
+    ctx.set_profiling(True)
+    ctx.stage_times()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    st = ctx.stage_times()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    total_sq = B * world * args.steps
+    value = total_sq / el
+    stages = stage_report(st, k, B)
+    dom = max((s for s in stages if "achieved" in stages[s]), key=lambda s: stages[s]["avg_ms"])
+    d = stages[dom]
+    roofline = {"bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"], "unit": d["unit"],
+                "frac": d["frac"], "traffic": load_traffic(dom), "kernel": dom}
+    rs_ms = sum(stages[s]["avg_ms"] for s in ("rs_q0", "rs_q3") if s in stages)
+    rs_roof = {"bound": "hbm", "achieved": rs_bytes(k) * B / (rs_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+               "unit": "GB/s"}
+    rs_roof["frac"] = rs_roof["achieved"] / rs_roof["peak"]
+
+    extras = {}
+    if rank == 0 and not args.no_extras:
+        # config 2: single-square latency at k=128 (one ProcessProposal)
+        lat = []
+        for _ in range(10):
+            torch.cuda.synchronize(dev)
+            a = time.perf_counter()
+            ctx.extend_dah_device(d_ods.data_ptr(), k, 1, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
+                                  d_roots.data_ptr(), d_status.data_ptr(), stream)
+            torch.cuda.synchronize(dev)
+            lat.append(time.perf_counter() - a)
+        extras["latency_single_square_ms"] = 1e3 * sorted(lat)[len(lat) // 2]
+        # config 3: one 512 x 512 square (GF(2^16), 512 MiB EDS)
+        del d_eds
+        torch.cuda.empty_cache()
+        k5 = 512
+        o5 = torch.from_numpy(testfactory.random_square(k5, 0)).to(dev)
+        e5 = torch.empty(4 * k5 * k5 * SHARE, dtype=torch.uint8, device=dev)
+        r5 = torch.empty(2 * k5 * 90, dtype=torch.uint8, device=dev)
+        c5 = torch.empty(2 * k5 * 90, dtype=torch.uint8, device=dev)
+        g5 = torch.empty(32, dtype=torch.uint8, device=dev)
+
+        def step5():
+            ctx.extend_dah_device(o5.data_ptr(), k5, 1, e5.data_ptr(), r5.data_ptr(), c5.data_ptr(),
+                                  g5.data_ptr(), None, stream)
+        step5()
+        torch.cuda.synchronize(dev)
+        ctx.set_profiling(True)
+        ctx.stage_times()
+        n5 = 3
+        a = time.perf_counter()
+        for _ in range(n5):
+            step5()
+        torch.cuda.synchronize(dev)
+        el5 = time.perf_counter() - a
+        ctx.set_profiling(False)
+        extras["k512"] = {"squares_per_s": n5 / el5, "ms_per_square": 1e3 * el5 / n5,
+                          "ods_gb_per_s": n5 * k5 * k5 * SHARE / el5 / 1e9,
+                          "data_root": g5.cpu().numpy().tobytes().hex(),
+                          "stages": stage_report(ctx.stage_times(), k5, 1)}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
+
+    if rank == 0:
+        line = {
+            "metric": "EDS+DAH squares/sec (k=128)",
+            "value": value,
+            "unit": "squares/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * el / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/u32",
+            "data": "synthetic random-namespace squares (testfactory mirror, SplitMix64)",
+            "config": {"workload": f"k={k} ODS batch: {B} squares per GPU per step "
+                                   f"(config 2 shape; x8 GPUs = config 4's 1024)",
+                       "k": k, "squares_per_gpu_per_step": B, "parallelism": f"dp{world} (independent squares)"},
+            "ods_gb_per_s": value * k * k * SHARE / 1e9,
+            "roofline": roofline,
+            "rs_roofline": rs_roof,
+            "stages": stages,
+            "cpu_baseline": cpu,
+            "extras": extras,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

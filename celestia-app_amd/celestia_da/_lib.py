@@ -1,0 +1,155 @@
+"""ctypes binding of libcda.so (include/cda.h).
+
+The HIP library is the only compute path: if it cannot be loaded this module
+raises, there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("CDA_LIB", os.path.join(PKG_ROOT, "libcda.so"))
+
+SHARE_SIZE = 512
+NAMESPACE_SIZE = 29
+NMT_ROOT_SIZE = 90
+HASH_SIZE = 32
+
+CDA_OK = 0
+CDA_ERR_NOT_POW2 = -1
+CDA_ERR_CHUNK_SIZE = -2
+CDA_ERR_PUSH_ORDER = -3
+CDA_ERR_DEVICE = -4
+CDA_ERR_OOM = -5
+CDA_ERR_INVALID = -6
+CDA_ERR_UNSUPPORTED = -7
+
+EXPORTED = (
+    "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
+    "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
+    "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
+)
+STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
+
+
+class CdaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class PushOrderError(CdaError):
+    """nmt ErrInvalidPushOrder surfaced through RowRoots/ColRoots."""
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libcda.so and declare prototypes. Raises OSError if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"libcda.so not built at {LIB_PATH}; run __graft_entry__.build() "
+                          "(no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        u8p = C.POINTER(C.c_uint8)
+        vp = C.c_void_p
+        ctxp = C.c_void_p
+        L.cda_ctx_create.argtypes = [C.c_int, C.POINTER(ctxp)]
+        L.cda_ctx_destroy.argtypes = [ctxp]
+        L.cda_last_error.argtypes = [ctxp]
+        L.cda_last_error.restype = C.c_char_p
+        L.cda_version.restype = C.c_char_p
+        L.cda_extend_shares.argtypes = [ctxp, u8p, C.c_uint32, u8p]
+        L.cda_dah_from_eds.argtypes = [ctxp, u8p, C.c_uint32, u8p, u8p, u8p]
+        L.cda_extend_dah.argtypes = [ctxp, u8p, C.c_uint32, u8p, u8p, u8p, u8p]
+        L.cda_extend_dah_batch.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p, u8p,
+                                           C.POINTER(C.c_int32)]
+        L.cda_extend_dah_device.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.cda_rs_encode.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
+        L.cda_data_root.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p]
+        L.cda_push_order_detail.argtypes = [ctxp, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                            C.POINTER(C.c_uint32)]
+        L.cda_set_profiling.argtypes = [ctxp, C.c_int]
+        L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
+        _lib = L
+        return L
+
+
+def ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "buffers must be C-contiguous"
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+class Context:
+    """One libcda context (HIP device + stream)."""
+
+    def __init__(self, device: int = -1):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.cda_ctx_create(device, C.byref(h))
+        if rc != CDA_OK:
+            raise CdaError(rc, f"cda_ctx_create failed (rc={rc})")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cda_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int):
+        if rc == CDA_OK:
+            return
+        msg = self.lib.cda_last_error(self.h).decode()
+        if rc == CDA_ERR_PUSH_ORDER:
+            raise PushOrderError(rc, msg)
+        raise CdaError(rc, msg)
+
+    def set_profiling(self, on: bool):
+        self.check(self.lib.cda_set_profiling(self.h, 1 if on else 0))
+
+    def stage_times(self):
+        """{stage: (total_ms, launches)} since the previous call."""
+        ms = (C.c_double * len(STAGES))()
+        n = (C.c_uint32 * len(STAGES))()
+        self.check(self.lib.cda_stage_times(self.h, ms, n, len(STAGES)))
+        return {s: (ms[i], n[i]) for i, s in enumerate(STAGES)}
+
+    def extend_dah_device(self, d_ods: int, k: int, n: int, d_eds: int, d_rows: int, d_cols: int,
+                          d_roots: int, d_status: int | None = None, stream: int | None = None):
+        """Enqueue the whole path on device pointers (asynchronous)."""
+        self.check(self.lib.cda_extend_dah_device(self.h, d_ods, k, n, d_eds, d_rows, d_cols, d_roots,
+                                                  d_status, stream))
+
+    def push_order_detail(self):
+        a, i, p = C.c_int32(), C.c_uint32(), C.c_uint32()
+        self.lib.cda_push_order_detail(self.h, C.byref(a), C.byref(i), C.byref(p))
+        return a.value, i.value, p.value
+
+
+_default = None
+
+
+def default_context() -> Context:
+    global _default
+    with _lock:
+        pass
+    if _default is None:
+        _default = Context(int(os.environ.get("CDA_DEVICE", "-1")))
+    return _default

@@ -1,0 +1,94 @@
+// engine.h -- device runtime behind the C ABI: one context per GPU, owning a
+// HIP stream, the GF(2^16) tables and grow-only scratch buffers, and the
+// enqueue logic of the whole ODS -> EDS -> roots -> data-root pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cda_kernels.h"
+
+namespace cda {
+
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n);
+    void release();
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(ptr); }
+};
+
+class Engine {
+  public:
+    explicit Engine(int device);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    int init();                        // CDA_OK or CDA_ERR_*
+    std::mutex& mutex() { return mu_; }
+    const std::string& last_error() const { return err_; }
+    void clear_error() { err_.clear(); }
+    int fail(int code, const std::string& msg) { err_ = msg; return code; }
+    hipStream_t stream() const { return stream_; }
+
+    // Enqueue the full path for n squares of width k (device pointers).
+    // d_err: n u32 words (min-encoded push-order violation, ~0 = ordered);
+    // d_status (optional): n int32 CDA_OK / CDA_ERR_PUSH_ORDER.
+    int enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
+                           uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s);
+    // RS extension only (ExtendShares).
+    int enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s);
+    // Roots + data root of existing EDSs.
+    int enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots,
+                    uint32_t* d_err, int32_t* d_status, hipStream_t s);
+    int enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n, hipStream_t s);
+
+    // Host-buffer helpers (copy in, run, copy out, synchronise).
+    int host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
+                        uint8_t* roots, int32_t* status);
+    int host_extend(const uint8_t* ods, uint32_t k, uint8_t* eds);
+    int host_dah(const uint8_t* eds, uint32_t k, uint8_t* rows, uint8_t* cols, uint8_t* root);
+    int host_rs(const uint8_t* data, uint32_t k, uint32_t len, uint32_t n, uint8_t* parity);
+    int host_data_root(const uint8_t* rows, const uint8_t* cols, uint32_t w, uint8_t* root);
+
+    // Stage timing with HIP events on the launch stream (bench / profiling).
+    enum Stage { kStageRsQ0 = 0, kStageRsQ3, kStageOrder, kStageLeaves, kStageLevels, kStageDataRoot, kNumStages };
+    void set_profiling(bool on) { profiling_ = on; }
+    int collect_stage_times(double* ms, uint32_t* counts, int n);
+
+    int32_t po_axis = -1;
+    uint32_t po_index = 0, po_pos = 0;
+
+  private:
+    int check(hipError_t e, const char* what);
+    int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,
+                         bool src_is_eds);
+
+    struct Mark {
+        int stage;
+        hipEvent_t a, b;
+    };
+    void mark_begin(int stage, hipStream_t s);
+    void mark_end(hipStream_t s);
+    bool profiling_ = false;
+    std::vector<Mark> marks_;
+    std::vector<hipEvent_t> event_pool_;
+    double stage_ms_[kNumStages] = {};
+    uint32_t stage_n_[kNumStages] = {};
+    hipEvent_t take_event();
+
+    int device_;
+    hipStream_t stream_ = nullptr;
+    std::mutex mu_;
+    std::string err_;
+    DevBuf gf16_log_, gf16_exp_, gf16_skew_;
+    DevBuf leaf_, lvl_, root_slots_, err_buf_;
+    DevBuf h_ods_, h_eds_, h_rows_, h_cols_, h_roots_;   // device staging for host-buffer calls
+};
+
+}  // namespace cda

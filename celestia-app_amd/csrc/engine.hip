@@ -1,0 +1,344 @@
+// engine.hip -- implementation of cda::Engine (see engine.h).
+//
+// Pipeline per batch of n squares of width k (W = 2k), all on one stream:
+//   1. RS phase Q0: rows Q0->Q1 (+ Q0 copy into the EDS) and columns Q0->Q2
+//   2. RS phase Q3: rows Q2->Q3                     (rsmt2d erasureExtendSquare)
+//   3. Q0 namespace push-order check                (nmt Push, ErrInvalidPushOrder)
+//   4. leaf hashing, one per EDS cell               (NmtHasher.HashLeaf)
+//   5. log2(W) NMT levels over all 2W trees         (NmtHasher.HashNode)
+//   6. RFC-6962 data root                           (DataAvailabilityHeader.Hash)
+#include "engine.h"
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/cda.h"
+#include "leopard_tables.h"
+#include "sha256_dev.h"
+
+namespace cda {
+
+hipError_t DevBuf::ensure(size_t n) {
+    if (n <= bytes && ptr) return hipSuccess;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipMalloc(&ptr, want);
+    if (e != hipSuccess) {
+        ptr = nullptr;
+        bytes = 0;
+        return e;
+    }
+    bytes = want;
+    return hipSuccess;
+}
+
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+}
+
+Engine::Engine(int device) : device_(device) {}
+
+Engine::~Engine() {
+    if (device_ >= 0) (void)hipSetDevice(device_);
+    for (DevBuf* b : {&gf16_log_, &gf16_exp_, &gf16_skew_, &leaf_, &lvl_, &root_slots_, &err_buf_, &h_ods_, &h_eds_,
+                      &h_rows_, &h_cols_, &h_roots_})
+        b->release();
+    for (Mark& m : marks_) {
+        if (m.a) (void)hipEventDestroy(m.a);
+        if (m.b) (void)hipEventDestroy(m.b);
+    }
+    for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int Engine::check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return CDA_OK;
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    (void)hipGetLastError();  // clear sticky launch error state
+    return fail(e == hipErrorOutOfMemory ? CDA_ERR_OOM : CDA_ERR_DEVICE, buf);
+}
+
+int Engine::init() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(CDA_ERR_DEVICE, "no HIP device available");
+    if (device_ < 0) {
+        if (hipGetDevice(&device_) != hipSuccess) return fail(CDA_ERR_DEVICE, "hipGetDevice failed");
+    }
+    if (device_ >= n) return fail(CDA_ERR_INVALID, "device ordinal out of range");
+    int rc;
+    if ((rc = check(hipSetDevice(device_), "hipSetDevice"))) return rc;
+    if ((rc = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
+    auto F = std::make_unique<LeoField<16>>();
+    leo_build<16>(*F, 0x1002D, kCantor16);
+    if ((rc = check(gf16_log_.ensure(sizeof F->log), "hipMalloc"))) return rc;
+    if ((rc = check(gf16_exp_.ensure(sizeof F->exp), "hipMalloc"))) return rc;
+    if ((rc = check(gf16_skew_.ensure(sizeof F->skew), "hipMalloc"))) return rc;
+    if ((rc = check(hipMemcpy(gf16_log_.ptr, F->log, sizeof F->log, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
+    if ((rc = check(hipMemcpy(gf16_exp_.ptr, F->exp, sizeof F->exp, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
+    if ((rc = check(hipMemcpy(gf16_skew_.ptr, F->skew, sizeof F->skew, hipMemcpyHostToDevice), "hipMemcpy")))
+        return rc;
+    return CDA_OK;
+}
+
+static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+hipEvent_t Engine::take_event() {
+    if (!event_pool_.empty()) {
+        hipEvent_t e = event_pool_.back();
+        event_pool_.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void Engine::mark_begin(int stage, hipStream_t s) {
+    if (!profiling_) return;
+    Mark m{stage, take_event(), take_event()};
+    if (m.a) (void)hipEventRecord(m.a, s);
+    marks_.push_back(m);
+}
+
+void Engine::mark_end(hipStream_t s) {
+    if (!profiling_ || marks_.empty()) return;
+    if (marks_.back().b) (void)hipEventRecord(marks_.back().b, s);
+}
+
+int Engine::collect_stage_times(double* ms, uint32_t* counts, int n) {
+    for (Mark& m : marks_) {
+        if (m.a && m.b && hipEventSynchronize(m.b) == hipSuccess) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, m.a, m.b) == hipSuccess) {
+                stage_ms_[m.stage] += t;
+                stage_n_[m.stage] += 1;
+            }
+        }
+        if (m.a) event_pool_.push_back(m.a);
+        if (m.b) event_pool_.push_back(m.b);
+    }
+    marks_.clear();
+    for (int i = 0; i < n && i < kNumStages; i++) {
+        if (ms) ms[i] = stage_ms_[i];
+        if (counts) counts[i] = stage_n_[i];
+        stage_ms_[i] = 0;
+        stage_n_[i] = 0;
+    }
+    return CDA_OK;
+}
+
+int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s) {
+    if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
+    int rc;
+    if (k <= 128) {
+        mark_begin(kStageRsQ0, s);
+        if ((rc = check(launch_rs8(d_ods, d_eds, k, n, kPhaseQ0, s), "rs8 Q0"))) return rc;
+        mark_end(s);
+        mark_begin(kStageRsQ3, s);
+        if ((rc = check(launch_rs8(d_ods, d_eds, k, n, kPhaseQ3, s), "rs8 Q3"))) return rc;
+        mark_end(s);
+    } else {
+        Gf16Dev t{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
+        mark_begin(kStageRsQ0, s);
+        if ((rc = check(launch_rs16(t, d_ods, d_eds, k, n, kPhaseQ0, s), "rs16 Q0"))) return rc;
+        mark_end(s);
+        mark_begin(kStageRsQ3, s);
+        if ((rc = check(launch_rs16(t, d_ods, d_eds, k, n, kPhaseQ3, s), "rs16 Q3"))) return rc;
+        mark_end(s);
+    }
+    return CDA_OK;
+}
+
+int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols,
+                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s) {
+    if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
+    const uint32_t W = 2 * k;
+    const size_t slots = (size_t)n * W * W * kSlot;
+    int rc;
+    if ((rc = check(leaf_.ensure(slots), "hipMalloc leaf slots"))) return rc;
+    if ((rc = check(lvl_.ensure(slots), "hipMalloc level slots"))) return rc;
+    if ((rc = check(root_slots_.ensure((size_t)n * 2 * W * kSlot), "hipMalloc root slots"))) return rc;
+    if ((rc = check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync"))) return rc;
+    mark_begin(kStageOrder, s);
+    if ((rc = check(launch_order_check(d_eds, k, n, d_err, s), "order check"))) return rc;
+    mark_end(s);
+    mark_begin(kStageLeaves, s);
+    if ((rc = check(launch_leaves(d_eds, k, n, leaf_.as<uint8_t>(), s), "leaf hashing"))) return rc;
+    mark_end(s);
+    mark_begin(kStageLevels, s);
+    uint8_t* in = leaf_.as<uint8_t>();
+    uint8_t* out = lvl_.as<uint8_t>();
+    bool in_leaf = true;
+    for (uint32_t n_in = W; n_in >= 2; n_in /= 2) {
+        if ((rc = check(launch_level(in, in_leaf, W, n_in, n, out, d_rows, d_cols, root_slots_.as<uint8_t>(), s),
+                        "nmt level")))
+            return rc;
+        uint8_t* t = in;
+        in = out;
+        out = t;
+        in_leaf = false;
+    }
+    mark_end(s);
+    mark_begin(kStageDataRoot, s);
+    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), W, n, d_roots, s), "data root"))) return rc;
+    mark_end(s);
+    if (d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
+    return CDA_OK;
+}
+
+int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
+                               uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
+                               hipStream_t s) {
+    int rc = enqueue_extend(d_ods, k, n, d_eds, s);
+    if (rc) return rc;
+    return enqueue_dah(d_eds, k, n, d_rows, d_cols, d_roots, d_err, d_status, s);
+}
+
+int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n,
+                       hipStream_t s) {
+    if (len % 64) {
+        char buf[96];
+        snprintf(buf, sizeof buf, "chunkSize %u must be a multiple of 64 bytes", len);
+        return fail(CDA_ERR_CHUNK_SIZE, buf);
+    }
+    if (!pow2(k)) return fail(CDA_ERR_UNSUPPORTED, "shard count must be a power of two");
+    if (k == 1)
+        return check(hipMemcpyAsync(d_parity, d_data, (size_t)len * n, hipMemcpyDeviceToDevice, s), "copy");
+    if (k <= 128) return check(launch_rs8_flat(d_data, d_parity, k, len, n, s), "rs8 flat");
+    if (k > 1024) return fail(CDA_ERR_UNSUPPORTED, "more than 2048 shards");
+    Gf16Dev t{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
+    return check(launch_rs16_flat(t, d_data, d_parity, k, len, n, s), "rs16 flat");
+}
+
+// Build the reference's error text for the first violating square.
+int Engine::push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* src, uint32_t k,
+                             bool src_is_eds) {
+    for (uint32_t sq = 0; sq < n; sq++) {
+        const uint32_t e = err_words[sq];
+        if (e == 0xFFFFFFFFu) continue;
+        po_axis = (int32_t)(e >> 24);
+        po_index = (e >> 12) & 0xFFF;
+        po_pos = e & 0xFFF;
+        const uint32_t w = src_is_eds ? 2 * k : k;
+        const uint8_t* base = src + (size_t)sq * w * w * kShare;
+        auto cell = [&](uint32_t pos) {
+            const uint32_t r = po_axis == 0 ? po_index : pos, c = po_axis == 0 ? pos : po_index;
+            return base + ((size_t)r * w + c) * kShare;
+        };
+        std::string msg = "pushed data has to be lexicographically ordered by namespace IDs: last namespace: ";
+        char hx[3];
+        const uint8_t* last = cell(po_pos - 1);
+        const uint8_t* pushed = cell(po_pos);
+        for (int i = 0; i < kNs; i++) { snprintf(hx, sizeof hx, "%02x", last[i]); msg += hx; }
+        msg += ", pushed: ";
+        for (int i = 0; i < kNs; i++) { snprintf(hx, sizeof hx, "%02x", pushed[i]); msg += hx; }
+        return fail(CDA_ERR_PUSH_ORDER, msg);
+    }
+    return CDA_OK;
+}
+
+int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
+                            uint8_t* roots, int32_t* status) {
+    const uint32_t W = 2 * k;
+    const size_t ods_b = (size_t)n * k * k * kShare, eds_b = (size_t)n * W * W * kShare;
+    const size_t roots_b = (size_t)n * W * kNode;
+    int rc;
+    if ((rc = check(h_ods_.ensure(ods_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_eds_.ensure(eds_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_rows_.ensure(roots_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_cols_.ensure(roots_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_roots_.ensure((size_t)n * 32), "hipMalloc"))) return rc;
+    if ((rc = check(err_buf_.ensure((size_t)n * 4), "hipMalloc"))) return rc;
+    hipStream_t s = stream_;
+    if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
+    if ((rc = enqueue_extend_dah(h_ods_.as<uint8_t>(), k, n, h_eds_.as<uint8_t>(), h_rows_.as<uint8_t>(),
+                                 h_cols_.as<uint8_t>(), h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s)))
+        return rc;
+    if (eds && (rc = check(hipMemcpyAsync(eds, h_eds_.ptr, eds_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(rows, h_rows_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(cols, h_cols_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(roots, h_roots_.ptr, (size_t)n * 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    std::vector<uint32_t> err(n);
+    if ((rc = check(hipMemcpyAsync(err.data(), err_buf_.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H")))
+        return rc;
+    if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    if (status)
+        for (uint32_t i = 0; i < n; i++) status[i] = err[i] == 0xFFFFFFFFu ? CDA_OK : CDA_ERR_PUSH_ORDER;
+    return push_order_error(err.data(), n, ods, k, false);
+}
+
+int Engine::host_extend(const uint8_t* ods, uint32_t k, uint8_t* eds) {
+    const uint32_t W = 2 * k;
+    const size_t ods_b = (size_t)k * k * kShare, eds_b = (size_t)W * W * kShare;
+    int rc;
+    if ((rc = check(h_ods_.ensure(ods_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_eds_.ensure(eds_b), "hipMalloc"))) return rc;
+    hipStream_t s = stream_;
+    if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
+    if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, 1, h_eds_.as<uint8_t>(), s))) return rc;
+    if ((rc = check(hipMemcpyAsync(eds, h_eds_.ptr, eds_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    return check(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+int Engine::host_dah(const uint8_t* eds, uint32_t k, uint8_t* rows, uint8_t* cols, uint8_t* root) {
+    const uint32_t W = 2 * k;
+    const size_t eds_b = (size_t)W * W * kShare, roots_b = (size_t)W * kNode;
+    int rc;
+    if ((rc = check(h_eds_.ensure(eds_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_rows_.ensure(roots_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_cols_.ensure(roots_b), "hipMalloc"))) return rc;
+    if ((rc = check(h_roots_.ensure(32), "hipMalloc"))) return rc;
+    if ((rc = check(err_buf_.ensure(4), "hipMalloc"))) return rc;
+    hipStream_t s = stream_;
+    if ((rc = check(hipMemcpyAsync(h_eds_.ptr, eds, eds_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
+    if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, 1, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
+                          h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s)))
+        return rc;
+    uint32_t err = 0;
+    if ((rc = check(hipMemcpyAsync(rows, h_rows_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(cols, h_cols_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(root, h_roots_.ptr, 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(&err, err_buf_.ptr, 4, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    return push_order_error(&err, 1, eds, k, true);
+}
+
+int Engine::host_rs(const uint8_t* data, uint32_t k, uint32_t len, uint32_t n, uint8_t* parity) {
+    const size_t b = (size_t)n * k * len;
+    int rc;
+    if ((rc = check(h_ods_.ensure(b), "hipMalloc"))) return rc;
+    if ((rc = check(h_eds_.ensure(b), "hipMalloc"))) return rc;
+    hipStream_t s = stream_;
+    if ((rc = check(hipMemcpyAsync(h_ods_.ptr, data, b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
+    if ((rc = enqueue_rs(h_ods_.as<uint8_t>(), h_eds_.as<uint8_t>(), k, len, n, s))) return rc;
+    if ((rc = check(hipMemcpyAsync(parity, h_eds_.ptr, b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    return check(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+int Engine::host_data_root(const uint8_t* rows, const uint8_t* cols, uint32_t w, uint8_t* root) {
+    // Pack the 90-B roots into 96-B slots (rows then columns) and reuse the
+    // device RFC-6962 kernel.
+    std::vector<uint8_t> slots((size_t)2 * w * kSlot, 0);
+    for (uint32_t i = 0; i < w; i++) {
+        memcpy(&slots[(size_t)i * kSlot], rows + (size_t)i * kNode, kNode);
+        memcpy(&slots[(size_t)(w + i) * kSlot], cols + (size_t)i * kNode, kNode);
+    }
+    int rc;
+    if ((rc = check(root_slots_.ensure(slots.size()), "hipMalloc"))) return rc;
+    if ((rc = check(h_roots_.ensure(32), "hipMalloc"))) return rc;
+    hipStream_t s = stream_;
+    if ((rc = check(hipMemcpyAsync(root_slots_.ptr, slots.data(), slots.size(), hipMemcpyHostToDevice, s), "H2D")))
+        return rc;
+    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), w, 1, h_roots_.as<uint8_t>(), s), "data root")))
+        return rc;
+    if ((rc = check(hipMemcpyAsync(root, h_roots_.ptr, 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    return check(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+}  // namespace cda

@@ -1,0 +1,303 @@
+// nmt.hip -- namespaced Merkle roots of every EDS row/column and the data root.
+//
+// Reference behaviour (paths under /root/reference):
+//   * rsmt2d computeRoots (EXT v0.14.0), called from
+//     pkg/da/data_availability_header.go:45,49: one tree per row and column,
+//     W = 2k leaves pushed in order.
+//   * pkg/wrapper/nmt_wrapper.go:93-140: leaf namespace = share[0:29] in Q0,
+//     ParitySharesNamespace (0xFF*29) elsewhere; :97-99 short-data error.
+//   * nmt v0.22.0 (EXT; hasher rules copied in-tree at
+//     test/util/malicious/hasher.go:186-310): HashLeaf, HashNode,
+//     computeNsRange with IgnoreMaxNamespace(true); Push rejects a namespace
+//     smaller than the previous one (ErrInvalidPushOrder).
+//   * pkg/da/data_availability_header.go:92-108 -> go-square/merkle
+//     HashFromByteSlices (RFC-6962) over rowRoots || colRoots.
+//
+// MI355X mapping.  The quadrant test is symmetric in (row, col), so a cell's
+// leaf node is identical in its row tree and its column tree: it is hashed
+// once (4k^2 leaf hashes instead of the reference's 8k^2).  One thread per
+// leaf / per parent node; each NMT level of all 4k trees of every square in
+// the batch is one launch.  SHA-256 is pure 32-bit VALU work (no MFMA).
+#include "cda_kernels.h"
+#include "sha256_dev.h"
+
+namespace cda {
+
+namespace {
+
+constexpr size_t SH = 512;
+
+__device__ __forceinline__ void load_chunk(const uint4* p, uint32_t (&w)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 v = p[q];
+        w[4 * q + 0] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+}
+__device__ __forceinline__ void bswap16(uint32_t (&w)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);
+}
+__device__ __forceinline__ void load_slot_be(const uint8_t* slot, uint32_t (&w)[kSlotWords]) {
+    const uint4* p = reinterpret_cast<const uint4*>(slot);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const uint4 v = p[q];
+        w[4 * q + 0] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y);
+        w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
+    }
+}
+__device__ __forceinline__ void store_slot(uint8_t* slot, const uint32_t (&w)[kSlotWords]) {
+    uint4* p = reinterpret_cast<uint4*>(slot);
+#pragma unroll
+    for (int q = 0; q < 6; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+// ---------------------------------------------------------------------------
+// Q0 push-order check (nmt ErrInvalidPushOrder on any row or column of Q0).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_ns_be(const uint8_t* cell, uint32_t (&ns)[8]) {
+    const uint4* p = reinterpret_cast<const uint4*>(cell);
+    const uint4 a = p[0], b = p[1];
+    ns[0] = bswap32(a.x); ns[1] = bswap32(a.y); ns[2] = bswap32(a.z); ns[3] = bswap32(a.w);
+    ns[4] = bswap32(b.x); ns[5] = bswap32(b.y); ns[6] = bswap32(b.z); ns[7] = bswap32(b.w) & 0xFF000000u;
+}
+// a < b lexicographically over the 29 namespace bytes
+__device__ __forceinline__ bool ns_less(const uint32_t (&a)[8], const uint32_t (&b)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (a[i] != b[i]) return a[i] < b[i];
+    return false;
+}
+
+__global__ __launch_bounds__(256) void order_kernel(const uint8_t* __restrict__ eds, uint32_t k,
+                                                   uint32_t* __restrict__ err) {
+    const uint32_t W = 2 * k;
+    const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
+    if (cell >= k * k) return;
+    const size_t sq = blockIdx.y;
+    const uint32_t r = cell / k, c = cell % k;
+    const uint8_t* E = eds + sq * (size_t)W * W * SH;
+    uint32_t me[8], nb[8];
+    load_ns_be(E + ((size_t)r * W + c) * SH, me);
+    uint32_t key = 0xFFFFFFFFu;
+    if (c + 1 < k) {
+        load_ns_be(E + ((size_t)r * W + c + 1) * SH, nb);
+        if (ns_less(nb, me)) key = min(key, (0u << 24) | (r << 12) | (c + 1));
+    }
+    if (r + 1 < k) {
+        load_ns_be(E + ((size_t)(r + 1) * W + c) * SH, nb);
+        if (ns_less(nb, me)) key = min(key, (1u << 24) | (c << 12) | (r + 1));
+    }
+    if (key != 0xFFFFFFFFu) atomicMin(err + sq, key);
+}
+
+// ---------------------------------------------------------------------------
+// Leaf hashing: one thread per EDS cell, 9 SHA-256 blocks of
+// 0x00 || ns || share, share streamed in 64-B chunks (prefetch one ahead).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void leaf_kernel(const uint8_t* __restrict__ eds, uint32_t k,
+                                                  uint8_t* __restrict__ slots) {
+    const uint32_t W = 2 * k;
+    const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
+    if (cell >= W * W) return;
+    const size_t sq = blockIdx.y;
+    const uint32_t r = cell / W, c = cell % W;
+    const bool parity = !(r < k && c < k);
+    const uint4* src = reinterpret_cast<const uint4*>(eds + (sq * (size_t)W * W + cell) * SH);
+
+    ShaState st;
+    sha_init(st);
+    uint32_t prev[16], cur[16], nxt[16], w[16], nsw[8];
+    load_chunk(src, cur);
+    load_chunk(src + 4, nxt);
+    bswap16(cur);
+#pragma unroll
+    for (int i = 0; i < 8; i++) nsw[i] = parity ? 0xFFFFFFFFu : cur[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) w[i] = leaf_msg_head(cur, parity, i);
+#pragma unroll
+    for (int i = 8; i < 16; i++) w[i] = leaf_msg_body(cur[i - 8], cur[i - 7]);
+    sha_compress(st, w);
+
+#pragma unroll 1
+    for (int b = 1; b < 8; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = cur[i];
+#pragma unroll
+        for (int i = 0; i < 16; i++) cur[i] = bswap32(nxt[i]);
+        if (b < 7) load_chunk(src + 4 * (b + 1), nxt);
+#pragma unroll
+        for (int t = 0; t < 7; t++) w[t] = leaf_msg_body(prev[8 + t], prev[9 + t]);
+        w[7] = leaf_msg_body(prev[15], cur[0]);
+#pragma unroll
+        for (int t = 8; t < 16; t++) w[t] = leaf_msg_body(cur[t - 8], cur[t - 7]);
+        sha_compress(st, w);
+    }
+    // block 8: share words 120..127 then padding
+#pragma unroll
+    for (int t = 0; t < 7; t++) w[t] = leaf_msg_body(cur[8 + t], cur[9 + t]);
+    w[7] = (cur[15] << 16) | 0x8000u;
+#pragma unroll
+    for (int t = 8; t < 15; t++) w[t] = 0;
+    w[15] = kLeafMsgBits;
+    sha_compress(st, w);
+
+    uint32_t out[kSlotWords];
+    leaf_node_words(nsw, st.h, out);
+    store_slot(slots + (sq * (size_t)W * W + cell) * kSlot, out);
+}
+
+// ---------------------------------------------------------------------------
+// One NMT level.  blockIdx.z = axis (0 rows, 1 columns).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void level_kernel(const uint8_t* __restrict__ in, int in_leaf, uint32_t W,
+                                                   uint32_t n_in, uint8_t* __restrict__ out,
+                                                   uint8_t* __restrict__ row_roots, uint8_t* __restrict__ col_roots,
+                                                   uint8_t* __restrict__ root_slots) {
+    const uint32_t n_out = n_in / 2;
+    const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= W * n_out) return;
+    const uint32_t axis = blockIdx.z;
+    const size_t sq = blockIdx.y;
+    uint32_t t, p;
+    const uint8_t *l, *rr;
+    if (in_leaf) {
+        const uint8_t* base = in + sq * (size_t)W * W * kSlot;
+        if (axis == 0) {  // row tree t: leaves (t, i)
+            t = idx / n_out; p = idx % n_out;
+            l = base + ((size_t)t * W + 2 * p) * kSlot;
+            rr = l + kSlot;
+        } else {          // column tree t: leaves (i, t); consecutive threads = consecutive trees
+            p = idx / W; t = idx % W;
+            l = base + ((size_t)(2 * p) * W + t) * kSlot;
+            rr = l + (size_t)W * kSlot;
+        }
+    } else {
+        t = idx / n_out; p = idx % n_out;
+        l = in + ((sq * 2 + axis) * W + t) * (size_t)n_in * kSlot + (size_t)(2 * p) * kSlot;
+        rr = l + kSlot;
+    }
+    uint32_t L[kSlotWords], R[kSlotWords], w[16];
+    load_slot_be(l, L);
+    load_slot_be(rr, R);
+    ShaState st;
+    sha_init(st);
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
+        sha_compress(st, w);
+    }
+    uint32_t o[kSlotWords];
+    inner_node_words(L, R, st.h, o);
+    if (n_out == 1) {
+        uint8_t* dst = (axis == 0 ? row_roots : col_roots) + (sq * W + t) * (size_t)kNode;
+        uint16_t* d16 = reinterpret_cast<uint16_t*>(dst);   // 90-byte packed roots are 2-B aligned
+#pragma unroll
+        for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
+        store_slot(root_slots + ((sq * 2 + axis) * W + t) * (size_t)kSlot, o);
+    } else {
+        store_slot(out + ((sq * 2 + axis) * W + t) * (size_t)n_out * kSlot + (size_t)p * kSlot, o);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Data root: RFC-6962 over the 2W root slots (rows then columns); 2W is a
+// power of two so the tree is perfect.  One 256-thread block per square.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void data_root_kernel(const uint8_t* __restrict__ root_slots, uint32_t W,
+                                                       uint8_t* __restrict__ data_roots) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // ping [2W][8] | pong [W][8]
+    const size_t sq = blockIdx.x;
+    const uint32_t n = 2 * W;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t I[kSlotWords], w[16];
+        load_slot_be(root_slots + (sq * n + i) * (size_t)kSlot, I);
+        ShaState st;
+        sha_init(st);
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
+            sha_compress(st, w);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) hs[i * 8 + j] = st.h[j];
+    }
+    __syncthreads();
+    uint32_t* src = hs;
+    uint32_t* dst = hs + n * 8;
+    for (uint32_t m = n / 2; m >= 1; m >>= 1) {
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            uint32_t A[8], B[8], w[16];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { A[j] = src[(2 * i) * 8 + j]; B[j] = src[(2 * i + 1) * 8 + j]; }
+            ShaState st;
+            sha_init(st);
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(A, B, 16 * b + j);
+                sha_compress(st, w);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) dst[i * 8 + j] = st.h[j];
+        }
+        __syncthreads();
+        uint32_t* t = src; src = dst; dst = t;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(data_roots + sq * 32);
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = bswap32(src[j]);
+    }
+}
+
+__global__ void status_kernel(const uint32_t* __restrict__ err, uint32_t n, int32_t* __restrict__ status) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) status[i] = err[i] == 0xFFFFFFFFu ? 0 : -3;   // CDA_OK / CDA_ERR_PUSH_ORDER
+}
+
+}  // namespace
+
+hipError_t launch_status(const uint32_t* err, uint32_t n, int32_t* status, hipStream_t s) {
+    hipLaunchKernelGGL(status_kernel, dim3((n + 255) / 256), dim3(256), 0, s, err, n, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_order_check(const uint8_t* eds, uint32_t k, uint32_t n, uint32_t* err, hipStream_t s) {
+    dim3 grid((k * k + 255) / 256, n);
+    hipLaunchKernelGGL(order_kernel, grid, dim3(256), 0, s, eds, k, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n, uint8_t* slots, hipStream_t s) {
+    const uint32_t W = 2 * k;
+    dim3 grid((W * W + 255) / 256, n);
+    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), 0, s, eds, k, slots);
+    return hipGetLastError();
+}
+
+hipError_t launch_level(const uint8_t* in, bool in_leaf, uint32_t W, uint32_t n_in, uint32_t n, uint8_t* out,
+                        uint8_t* row_roots, uint8_t* col_roots, uint8_t* root_slots, hipStream_t s) {
+    const uint32_t per_axis = W * (n_in / 2);
+    dim3 grid((per_axis + 255) / 256, n, 2);
+    hipLaunchKernelGGL(level_kernel, grid, dim3(256), 0, s, in, in_leaf ? 1 : 0, W, n_in, out, row_roots, col_roots,
+                       root_slots);
+    return hipGetLastError();
+}
+
+hipError_t launch_data_root(const uint8_t* root_slots, uint32_t W, uint32_t n, uint8_t* data_roots, hipStream_t s) {
+    const size_t lds = (size_t)3 * W * 32;   // ping-pong: 2W + W digests
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(data_root_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(data_root_kernel, dim3(n), dim3(256), lds, s, root_slots, W, data_roots);
+    return hipGetLastError();
+}
+
+}  // namespace cda

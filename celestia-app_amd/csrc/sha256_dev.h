@@ -1,0 +1,188 @@
+// sha256_dev.h -- SHA-256 compression and NMT message/node builders.
+//
+// Everything here is plain C++ on 32-bit words (rotates and byte funnels are
+// written so LLVM selects v_alignbit_b32 / v_alignbyte_b32 / v_bitop3_b32 on
+// gfx950), marked __host__ __device__ so tests/cpp can check the byte layouts
+// on the CPU against the oracle before a kernel runs.
+//
+// Byte layouts follow the nmt hasher (in-tree copy
+// /root/reference/test/util/malicious/hasher.go:186-310) and the erasured
+// wrapper (/root/reference/pkg/wrapper/nmt_wrapper.go:93-140):
+//   leaf message  = 0x00 || ns(29) || share(512)              (542 B, 9 blocks)
+//   leaf node     = ns || ns || sha256(leaf message)          (90 B)
+//   inner message = 0x01 || left(90) || right(90)             (181 B, 3 blocks)
+//   inner node    = l.min || (r.min == 0xFF*29 ? l.max : r.max) || sha256(...)
+// Nodes are kept on device in 96-byte slots (90 B + 6 zero bytes) so every
+// node load/store is 16-byte aligned.
+#pragma once
+#include <stdint.h>
+
+#ifndef CDA_HD
+#define CDA_HD __host__ __device__ __forceinline__
+#endif
+
+namespace cda {
+
+constexpr int kShare = 512;
+constexpr int kNs = 29;
+constexpr int kNode = 90;
+constexpr int kSlot = 96;       // device node slot (bytes)
+constexpr int kSlotWords = 24;
+
+CDA_HD uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+// ({hi, lo} >> 8*s)[31:0]  -> v_alignbyte_b32
+CDA_HD uint32_t funnel8(uint32_t hi, uint32_t lo, int s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * s));
+}
+CDA_HD uint32_t bswap32(uint32_t x) {
+    return (x >> 24) | ((x >> 8) & 0x0000FF00u) | ((x << 8) & 0x00FF0000u) | (x << 24);
+}
+
+struct ShaState {
+    uint32_t h[8];
+};
+
+CDA_HD void sha_init(ShaState& s) {
+    s.h[0] = 0x6a09e667u; s.h[1] = 0xbb67ae85u; s.h[2] = 0x3c6ef372u; s.h[3] = 0xa54ff53au;
+    s.h[4] = 0x510e527fu; s.h[5] = 0x9b05688cu; s.h[6] = 0x1f83d9abu; s.h[7] = 0x5be0cd19u;
+}
+
+#define CDA_SHA_K                                                                                        \
+    {0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u, \
+     0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u, \
+     0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, \
+     0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, \
+     0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, \
+     0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, \
+     0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u, \
+     0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u}
+
+// One compression; w[] holds the 16 big-endian message words and is consumed.
+CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+    uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+            uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            w[i & 15] = wi;
+        }
+        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        uint32_t ch = (e & f) ^ (~e & g);
+        uint32_t t1 = h + S1 + ch + K[i] + wi;
+        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+// ---------------------------------------------------------------------------
+// Leaf: message word i (big-endian) of 0x00 || ns || share, given the share as
+// big-endian words S[0..127] and `parity` (ns = 0xFF*29 instead of share[0:29]).
+// Block b needs S[16b-8 .. 16b+8].
+// ---------------------------------------------------------------------------
+CDA_HD uint32_t leaf_msg_head(const uint32_t* S, bool parity, int i) {   // i in 0..7
+    if (parity) {
+        if (i == 0) return 0x00FFFFFFu;
+        if (i < 7) return 0xFFFFFFFFu;
+        return 0xFFFF0000u | (S[0] >> 16);
+    }
+    if (i == 0) return S[0] >> 8;
+    if (i < 7) return funnel8(S[i - 1], S[i], 1);
+    return (S[6] << 24) | ((S[7] >> 24) << 16) | (S[0] >> 16);
+}
+// i in 8..134: bytes 4i.. = share[4i-30 ..]
+CDA_HD uint32_t leaf_msg_body(uint32_t s_im8, uint32_t s_im7) { return funnel8(s_im8, s_im7, 2); }
+constexpr uint32_t kLeafMsgBits = 542 * 8;
+
+// Leaf node slot words (little-endian u32 as stored in memory), from the ns
+// big-endian words NSW[0..7] (byte 28 = NSW[7] >> 24) and digest D[0..7].
+CDA_HD void leaf_node_words(const uint32_t NSW[8], const uint32_t D[8], uint32_t out[kSlotWords]) {
+    uint32_t be[kSlotWords];
+#pragma unroll
+    for (int t = 0; t < 7; t++) be[t] = NSW[t];
+    be[7] = (NSW[7] & 0xFF000000u) | (NSW[0] >> 8);
+#pragma unroll
+    for (int t = 8; t < 14; t++) be[t] = funnel8(NSW[t - 8], NSW[t - 7], 1);
+    be[14] = (NSW[6] << 24) | ((NSW[7] >> 24) << 16) | (D[0] >> 16);
+#pragma unroll
+    for (int t = 15; t < 22; t++) be[t] = funnel8(D[t - 15], D[t - 14], 2);
+    be[22] = D[7] << 16;
+    be[23] = 0;
+#pragma unroll
+    for (int t = 0; t < kSlotWords; t++) out[t] = bswap32(be[t]);
+}
+
+// ---------------------------------------------------------------------------
+// Inner node: L, R = big-endian words of the two child slots.  Message word i
+// of 0x01 || l(90) || r(90) (181 B, 3 blocks = 48 words).
+// ---------------------------------------------------------------------------
+CDA_HD uint32_t node_msg(const uint32_t* L, const uint32_t* R, int i) {
+    if (i == 0) return 0x01000000u | (L[0] >> 8);
+    if (i < 22) return funnel8(L[i - 1], L[i], 1);
+    if (i == 22) return (funnel8(L[21], L[22], 1) & 0xFFFFFF00u) | (R[0] >> 24);
+    if (i < 45) return funnel8(R[i - 23], R[i - 22], 3);
+    if (i == 45) return (R[22] << 8) | 0x00800000u;
+    if (i == 47) return 181u * 8u;
+    return 0;
+}
+
+CDA_HD bool is_parity_min(const uint32_t* R) {
+    bool all = true;
+#pragma unroll
+    for (int t = 0; t < 7; t++) all = all && (R[t] == 0xFFFFFFFFu);
+    return all && ((R[7] >> 24) == 0xFFu);
+}
+
+// Parent slot (little-endian words) from child big-endian words and digest.
+CDA_HD void inner_node_words(const uint32_t* L, const uint32_t* R, const uint32_t D[8], uint32_t out[kSlotWords]) {
+    const bool ign = is_parity_min(R);     // IgnoreMaxNamespace(true)
+    uint32_t be[kSlotWords];
+#pragma unroll
+    for (int t = 0; t < 7; t++) be[t] = L[t];
+    uint32_t x7 = ign ? L[7] : R[7];
+    be[7] = (L[7] & 0xFF000000u) | (x7 & 0x00FFFFFFu);
+#pragma unroll
+    for (int t = 8; t < 14; t++) be[t] = ign ? L[t] : R[t];
+    uint32_t x14 = ign ? L[14] : R[14];
+    be[14] = (x14 & 0xFFFF0000u) | (D[0] >> 16);
+#pragma unroll
+    for (int t = 15; t < 22; t++) be[t] = funnel8(D[t - 15], D[t - 14], 2);
+    be[22] = D[7] << 16;
+    be[23] = 0;
+#pragma unroll
+    for (int t = 0; t < kSlotWords; t++) out[t] = bswap32(be[t]);
+}
+
+// ---------------------------------------------------------------------------
+// RFC-6962 (go-square/merkle): leaf = sha256(0x00 || item90), inner =
+// sha256(0x01 || a32 || b32).  I = big-endian words of a 96-B slot.
+// ---------------------------------------------------------------------------
+CDA_HD uint32_t rfc_leaf_msg(const uint32_t* I, int i) {   // 91 B, 2 blocks
+    if (i == 0) return I[0] >> 8;
+    if (i < 22) return funnel8(I[i - 1], I[i], 1);
+    if (i == 22) return (funnel8(I[21], I[22], 1) & 0xFFFFFF00u) | 0x80u;
+    if (i == 31) return 91u * 8u;
+    return 0;
+}
+CDA_HD uint32_t rfc_inner_msg(const uint32_t* A, const uint32_t* B, int i) {   // 65 B, 2 blocks
+    if (i == 0) return 0x01000000u | (A[0] >> 8);
+    if (i < 8) return funnel8(A[i - 1], A[i], 1);
+    if (i == 8) return (A[7] << 24) | (B[0] >> 8);
+    if (i < 16) return funnel8(B[i - 9], B[i - 8], 1);
+    if (i == 16) return (B[7] << 24) | 0x00800000u;
+    if (i == 31) return 65u * 8u;
+    return 0;
+}
+
+}  // namespace cda

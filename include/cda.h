@@ -1,0 +1,132 @@
+/*
+ * cda.h -- C ABI of libcda.so, the MI355X (gfx950) implementation of
+ * celestia-app's block data-availability hot path:
+ *
+ *   ODS (k x k shares of 512 B) -> EDS (2k x 2k, Leopard RS) -> 4k NMT
+ *   row/column roots -> DataAvailabilityHeader data root.
+ *
+ * Every entry point replaces one reference interface (paths relative to the
+ * celestia-app v3 tree; EXT = third-party Go module pinned in go.mod):
+ *
+ *   cda_extend_shares      da.ExtendShares            pkg/da/data_availability_header.go:65-75
+ *   cda_dah_from_eds       da.NewDataAvailabilityHeader pkg/da/data_availability_header.go:44-63
+ *                          (+ rsmt2d (*EDS).RowRoots/ColRoots via
+ *                          wrapper.NewConstructor, pkg/wrapper/nmt_wrapper.go:73-86)
+ *   cda_extend_dah         ExtendShares + NewDataAvailabilityHeader in one
+ *                          submission (app/prepare_proposal.go:61,71;
+ *                          app/process_proposal.go:138,144)
+ *   cda_extend_dah_batch   the same for n independent squares
+ *   cda_rs_encode          rsmt2d Codec.Encode (appconsts.DefaultCodec,
+ *                          pkg/appconsts/global_consts.go:92 -> LeoRSCodec)
+ *   cda_data_root          (*DataAvailabilityHeader).Hash
+ *                          pkg/da/data_availability_header.go:92-108
+ *   cda_extend_dah_device  device-resident batch (inputs/outputs in HBM)
+ *
+ * Conventions
+ *   - All buffers are plain byte arrays; shares are row-major and contiguous
+ *     (share (r, c) of a width-w square at offset (r*w + c)*512).  NMT roots
+ *     are 90 bytes (min ns 29 || max ns 29 || sha256 32), packed.
+ *   - Inputs are borrowed for the duration of the call; outputs are written to
+ *     caller-owned buffers; the library keeps no pointer after return.
+ *   - Return value: CDA_OK (0) or a negative CDA_ERR_* code.  The message of
+ *     the last error on a context is available from cda_last_error(); it uses
+ *     the reference's error text where one exists.  The library never aborts
+ *     across the ABI.
+ *   - A context owns one HIP device and stream; calls on one context are
+ *     serialised by an internal mutex (rsmt2d calls Codec/Tree from many
+ *     goroutines).  Use one context per device.
+ */
+#ifndef CDA_H
+#define CDA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CDA_SHARE_SIZE 512     /* appconsts.ShareSize, pkg/appconsts/global_consts.go:29 */
+#define CDA_NAMESPACE_SIZE 29  /* appconsts.NamespaceSize, global_consts.go:26 */
+#define CDA_NMT_ROOT_SIZE 90   /* 2*NamespaceSize + sha256.Size */
+#define CDA_HASH_SIZE 32
+
+enum {
+    CDA_OK = 0,
+    CDA_ERR_NOT_POW2 = -1,      /* "number of shares is not a power of 2: got %d" (data_availability_header.go:68) */
+    CDA_ERR_CHUNK_SIZE = -2,    /* rsmt2d LeoRSCodec.ValidateChunkSize: "chunkSize %v must be a multiple of 64 bytes" */
+    CDA_ERR_PUSH_ORDER = -3,    /* nmt ErrInvalidPushOrder on a Q0 row/column (surfaces from RowRoots/ColRoots) */
+    CDA_ERR_DEVICE = -4,        /* HIP runtime / kernel launch failure */
+    CDA_ERR_OOM = -5,           /* device allocation failure */
+    CDA_ERR_INVALID = -6,       /* bad argument (NULL pointer, k out of range, ...) */
+    CDA_ERR_UNSUPPORTED = -7    /* shard count the codec does not support */
+};
+
+typedef struct cda_ctx cda_ctx;
+
+/* Context lifecycle. device: HIP ordinal (-1 = current device). */
+int cda_ctx_create(int device, cda_ctx **out);
+int cda_ctx_destroy(cda_ctx *ctx);
+/* Message of the last failed call on ctx (never NULL; "" after success). */
+const char *cda_last_error(cda_ctx *ctx);
+/* Library version string, e.g. "cda 0.1.0 gfx950". */
+const char *cda_version(void);
+
+/* da.ExtendShares: ods = k*k*512 bytes (k a power of two, k >= 1);
+ * eds = (2k)^2*512 bytes. n_shares is len(s) (checked for power of two). */
+int cda_extend_shares(cda_ctx *ctx, const uint8_t *ods, uint32_t n_shares, uint8_t *eds);
+
+/* da.NewDataAvailabilityHeader on an existing EDS of width w = 2k:
+ * row_roots, col_roots = w*90 bytes each; data_root = 32 bytes (DAH.Hash()).
+ * Returns CDA_ERR_PUSH_ORDER if a Q0 row or column is not namespace ordered. */
+int cda_dah_from_eds(cda_ctx *ctx, const uint8_t *eds, uint32_t w, uint8_t *row_roots, uint8_t *col_roots,
+                     uint8_t *data_root);
+
+/* ExtendShares + NewDataAvailabilityHeader in one device submission. eds may be
+ * NULL when the caller only needs the roots. On CDA_ERR_PUSH_ORDER the EDS is
+ * still written (ExtendShares succeeds; the error belongs to the DAH step). */
+int cda_extend_dah(cda_ctx *ctx, const uint8_t *ods, uint32_t n_shares, uint8_t *eds, uint8_t *row_roots,
+                   uint8_t *col_roots, uint8_t *data_root);
+
+/* Batch of n squares of width k, contiguous: ods = n*k*k*512, eds = n*(2k)^2*512
+ * (or NULL), row_roots/col_roots = n*2k*90, data_roots = n*32. status (may be
+ * NULL) receives one CDA_OK / CDA_ERR_PUSH_ORDER per square; the call returns
+ * CDA_ERR_PUSH_ORDER if any square failed. */
+int cda_extend_dah_batch(cda_ctx *ctx, const uint8_t *ods, uint32_t k, uint32_t n, uint8_t *eds, uint8_t *row_roots,
+                         uint8_t *col_roots, uint8_t *data_roots, int32_t *status);
+
+/* Device-resident batch: every pointer is device memory on ctx's device;
+ * stream is a hipStream_t (NULL = the context's stream). Asynchronous: the
+ * call only enqueues work. Per-square push-order status is written to d_status
+ * (n int32, device memory, may be NULL). */
+int cda_extend_dah_device(cda_ctx *ctx, const void *d_ods, uint32_t k, uint32_t n, void *d_eds, void *d_row_roots,
+                          void *d_col_roots, void *d_data_roots, int32_t *d_status, void *stream);
+
+/* rsmt2d Codec.Encode (Leopard, GF(2^8) for 2*n_shards <= 256, else GF(2^16)):
+ * n_codewords codewords, each n_shards data shards of shard_len bytes,
+ * contiguous; parity has the same shape. n_shards a power of two. */
+int cda_rs_encode(cda_ctx *ctx, const uint8_t *data, uint32_t n_shards, uint32_t shard_len, uint32_t n_codewords,
+                  uint8_t *parity);
+
+/* (*DataAvailabilityHeader).Hash: RFC-6962 root of row_roots || col_roots
+ * (w roots of 90 bytes each). w == 0 gives sha256("") like Hash() on a nil DAH. */
+int cda_data_root(cda_ctx *ctx, const uint8_t *row_roots, const uint8_t *col_roots, uint32_t w, uint8_t *data_root);
+
+/* Details of the last CDA_ERR_PUSH_ORDER on ctx: axis (0 row, 1 column), the
+ * axis index, and the leaf position whose push failed. */
+int cda_push_order_detail(cda_ctx *ctx, int32_t *axis, uint32_t *index, uint32_t *position);
+
+/* Stage timing (HIP events on the launch stream).  When enabled, every
+ * enqueued stage is bracketed by events; cda_stage_times synchronises them and
+ * returns, per stage, the summed milliseconds and launch counts since the
+ * previous call, then resets.  Stages: 0 RS Q0 (rows+cols), 1 RS Q3, 2 push-
+ * order check, 3 NMT leaves, 4 NMT levels, 5 data root. */
+#define CDA_NUM_STAGES 6
+int cda_set_profiling(cda_ctx *ctx, int enable);
+int cda_stage_times(cda_ctx *ctx, double *ms, uint32_t *counts, int n_stages);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CDA_H */
