@@ -1,9 +1,9 @@
 // sha256_dev.h -- SHA-256 compression and NMT message/node builders.
 //
-// Everything here is plain C++ on 32-bit words (rotates and byte funnels are
-// written so LLVM selects v_alignbit_b32 / v_alignbyte_b32 / v_bitop3_b32 on
-// gfx950), marked __host__ __device__ so tests/cpp can check the byte layouts
-// on the CPU against the oracle before a kernel runs.
+// Device code on 32-bit words.  The compression uses gfx950's three-input
+// integer ops explicitly: v_bitop3_b32 for XOR3 / Ch / Maj, v_add3_u32, and
+// v_alignbit_b32 rotates -- 14 VALU ops per round and 10 per schedule word,
+// 1384 per compression (DESIGN.md "SHA-256 op count").
 //
 // Byte layouts follow the nmt hasher (in-tree copy
 // /root/reference/test/util/malicious/hasher.go:186-310) and the erasured
@@ -18,7 +18,7 @@
 #include <stdint.h>
 
 #ifndef CDA_HD
-#define CDA_HD __host__ __device__ __forceinline__
+#define CDA_HD __device__ __forceinline__
 #endif
 
 namespace cda {
@@ -29,7 +29,12 @@ constexpr int kNode = 90;
 constexpr int kSlot = 96;       // device node slot (bytes)
 constexpr int kSlotWords = 24;
 
-CDA_HD uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+CDA_HD uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// v_bitop3_b32: result bit = imm[(a << 2) | (b << 1) | c]
+CDA_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+CDA_HD uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA); }
+CDA_HD uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8); }
+CDA_HD uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { return a + b + c; }
 // ({hi, lo} >> 8*s)[31:0]  -> v_alignbyte_b32
 CDA_HD uint32_t funnel8(uint32_t hi, uint32_t lo, int s) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * s));
@@ -69,18 +74,17 @@ CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
             wi = w[i];
         } else {
             uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-            uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
-            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wi = add3(w[i & 15], s0, w[(i - 7) & 15]) + s1;
             w[i & 15] = wi;
         }
-        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-        uint32_t ch = (e & f) ^ (~e & g);
-        uint32_t t1 = h + S1 + ch + K[i] + wi;
-        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        uint32_t t1 = add3(add3(h, S1, ch(e, f, g)), K[i], wi);
+        uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        uint32_t mj = maj(a, b, c);
         h = g; g = f; f = e; e = d + t1;
-        d = c; c = b; b = a; a = t1 + S0 + mj;
+        d = c; c = b; b = a; a = add3(t1, S0, mj);
     }
     s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
     s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
