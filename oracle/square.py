@@ -1,0 +1,305 @@
+"""Square construction (txs -> ODS) -- TEST INFRASTRUCTURE ONLY (oracle).
+
+Restates go-square v1.1.0 ``square.Construct`` (EXT module pinned at
+/root/reference/go.mod:9; not vendored) from the specs under
+/root/reference/specs/src/specs/: data_square_layout.md (blob share
+commitment rules, padding), shares.md (share format, compact and sparse
+shares, padding shares), namespace.md (reserved namespaces) and
+data_structures.md (IndexWrapper / BlobTx).  Call sites in the reference:
+app/prepare_proposal.go:50, app/process_proposal.go:122, app/extend_block.go:16.
+
+Its only job here is to pin the Leopard GF(2^8) restatement with real data:
+mainnet block 408 (x/blob/test/testdata/block_response.json, k = 32) has a
+data root that depends on real (non-constant) Reed-Solomon parity.
+"""
+from __future__ import annotations
+
+import base64
+import json
+import math
+
+SHARE_SIZE = 512
+NS_SIZE = 29
+SUBTREE_ROOT_THRESHOLD = 64          # pkg/appconsts/v1/app_consts.go
+
+TX_NS = b"\x00" * 28 + b"\x01"
+PFB_NS = b"\x00" * 28 + b"\x04"
+PRIMARY_RESERVED_PADDING_NS = b"\x00" * 28 + b"\xff"
+TAIL_PADDING_NS = b"\xff" * 28 + b"\xfe"
+
+
+# ---------------------------------------------------------------- protobuf
+def _varint(buf: bytes, i: int):
+    x, s = 0, 0
+    while True:
+        b = buf[i]
+        i += 1
+        x |= (b & 0x7F) << s
+        s += 7
+        if b < 0x80:
+            return x, i
+
+
+def _enc_varint(x: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = x & 0x7F
+        x >>= 7
+        if x:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _fields(buf: bytes):
+    i = 0
+    while i < len(buf):
+        key, i = _varint(buf, i)
+        fn, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _varint(buf, i)
+        elif wt == 2:
+            n, i = _varint(buf, i)
+            v = buf[i:i + n]
+            i += n
+        elif wt == 5:
+            v = buf[i:i + 4]
+            i += 4
+        elif wt == 1:
+            v = buf[i:i + 8]
+            i += 8
+        else:
+            raise ValueError("unsupported wire type")
+        yield fn, wt, v
+
+
+def unmarshal_blob_tx(tx: bytes):
+    """go-square tx.UnmarshalBlobTx: BlobTx{tx=1, blobs=2, type_id=3 == "BLOB"}."""
+    try:
+        inner, blobs, type_id = b"", [], b""
+        for fn, wt, v in _fields(tx):
+            if fn == 1 and wt == 2:
+                inner = v
+            elif fn == 2 and wt == 2:
+                blob = {"namespace_id": b"", "data": b"", "share_version": 0, "namespace_version": 0}
+                for bf, bw, bv in _fields(v):
+                    if bf == 1:
+                        blob["namespace_id"] = bv
+                    elif bf == 2:
+                        blob["data"] = bv
+                    elif bf == 3:
+                        blob["share_version"] = bv
+                    elif bf == 4:
+                        blob["namespace_version"] = bv
+                blobs.append(blob)
+            elif fn == 3 and wt == 2:
+                type_id = v
+    except Exception:
+        return None
+    if type_id != b"BLOB":
+        return None
+    return inner, blobs
+
+
+def marshal_index_wrapper(tx: bytes, share_indexes) -> bytes:
+    """IndexWrapper{tx=1, share_indexes=2 (packed), type_id=3 = "INDX"} (gogoproto order)."""
+    out = bytearray()
+    out += b"\x0a" + _enc_varint(len(tx)) + tx
+    if share_indexes:
+        packed = b"".join(_enc_varint(x) for x in share_indexes)
+        out += b"\x12" + _enc_varint(len(packed)) + packed
+    out += b"\x1a\x04INDX"
+    return bytes(out)
+
+
+# ------------------------------------------------------------------ shares
+def _info_byte(version: int, start: bool) -> int:
+    return (version << 1) | (1 if start else 0)
+
+
+def compact_shares(ns: bytes, units) -> list:
+    """CompactShareSplitter: varint-delimited units, reserved bytes = offset
+    of the first unit starting in the share (shares.md "Transaction Shares")."""
+    shares = []
+    cur = None
+    reserved_set = False
+
+    def new_share(first: bool):
+        b = bytearray(ns + bytes([_info_byte(0, first)]))
+        if first:
+            b += b"\x00" * 4           # sequence length, filled at export
+        res_at = len(b)
+        b += b"\x00" * 4               # reserved bytes
+        return b, res_at
+
+    res_at = 0
+    total = 0
+    for u in units:
+        data = _enc_varint(len(u)) + u
+        total += len(data)
+        if cur is None:
+            cur, res_at = new_share(True)
+            reserved_set = False
+        if not reserved_set:
+            cur[res_at:res_at + 4] = len(cur).to_bytes(4, "big")
+            reserved_set = True
+        while data:
+            room = SHARE_SIZE - len(cur)
+            cur += data[:room]
+            data = data[room:]
+            if len(cur) == SHARE_SIZE:
+                shares.append(cur)
+                cur, res_at = new_share(False)
+                reserved_set = False
+    if cur is not None and len(cur) > res_at + 4:
+        cur += b"\x00" * (SHARE_SIZE - len(cur))
+        shares.append(cur)
+    if shares:
+        shares[0][NS_SIZE + 1:NS_SIZE + 5] = total.to_bytes(4, "big")
+    return [bytes(s) for s in shares]
+
+
+def sparse_shares(ns: bytes, data: bytes, version: int = 0) -> list:
+    out = []
+    first = bytearray(ns + bytes([_info_byte(version, True)]) + len(data).to_bytes(4, "big"))
+    room = SHARE_SIZE - len(first)
+    first += data[:room]
+    data = data[room:]
+    out.append(first)
+    while data:
+        s = bytearray(ns + bytes([_info_byte(version, False)]))
+        room = SHARE_SIZE - len(s)
+        s += data[:room]
+        data = data[room:]
+        out.append(s)
+    return [bytes(s) + b"\x00" * (SHARE_SIZE - len(s)) for s in out]
+
+
+def padding_share(ns: bytes) -> bytes:
+    s = ns + bytes([_info_byte(0, True)]) + b"\x00" * 4
+    return s + b"\x00" * (SHARE_SIZE - len(s))
+
+
+def sparse_share_count(n_bytes: int) -> int:
+    if n_bytes <= SHARE_SIZE - NS_SIZE - 5:
+        return 1
+    rest = n_bytes - (SHARE_SIZE - NS_SIZE - 5)
+    return 1 + -(-rest // (SHARE_SIZE - NS_SIZE - 1))
+
+
+# ----------------------------------------------------------------- layout
+def round_up_pow2(x: int) -> int:
+    r = 1
+    while r < x:
+        r <<= 1
+    return r
+
+
+def blob_min_square_size(share_count: int) -> int:
+    return round_up_pow2(int(math.ceil(math.sqrt(share_count))))
+
+
+def subtree_width(share_count: int, threshold: int = SUBTREE_ROOT_THRESHOLD) -> int:
+    s = share_count // threshold + (1 if share_count % threshold else 0)
+    return min(round_up_pow2(s), blob_min_square_size(share_count))
+
+
+def next_share_index(cursor: int, blob_share_len: int, threshold: int = SUBTREE_ROOT_THRESHOLD) -> int:
+    w = subtree_width(blob_share_len, threshold)
+    return -(-cursor // w) * w
+
+
+FIRST_COMPACT_CONTENT = SHARE_SIZE - NS_SIZE - 1 - 4 - 4        # 474
+CONT_COMPACT_CONTENT = SHARE_SIZE - NS_SIZE - 1 - 4             # 478
+WORST_CASE_SHARE_INDEX = 128 * 128                               # worstCaseShareIndexes
+
+
+class CompactShareCounter:
+    """go-square shares.CompactShareCounter (share-count estimate)."""
+
+    def __init__(self):
+        self.shares = 0
+        self.remainder = 0
+
+    def add(self, data_len: int):
+        data_len += len(_enc_varint(data_len))
+        if self.shares == 0:
+            if data_len >= FIRST_COMPACT_CONTENT - self.remainder:
+                data_len -= FIRST_COMPACT_CONTENT - self.remainder
+                self.shares += 1
+                self.remainder = 0
+            else:
+                self.remainder += data_len
+                data_len = 0
+        if data_len >= CONT_COMPACT_CONTENT - self.remainder:
+            data_len -= CONT_COMPACT_CONTENT - self.remainder
+            self.shares += 1
+            self.remainder = 0
+        else:
+            self.remainder += data_len
+            data_len = 0
+        if data_len > 0:
+            self.shares += data_len // CONT_COMPACT_CONTENT
+            self.remainder = data_len % CONT_COMPACT_CONTENT
+
+    def size(self) -> int:
+        return self.shares if self.remainder == 0 else self.shares + 1
+
+
+def construct(txs, square_size: int, threshold: int = SUBTREE_ROOT_THRESHOLD) -> list:
+    """square.Construct (Builder.AppendTx / AppendBlobTx / Export / WriteSquare)
+    for the block's own square size."""
+    normal, pfbs, blobs = [], [], []
+    tx_counter, pfb_counter = CompactShareCounter(), CompactShareCounter()
+    for tx in txs:
+        bt = unmarshal_blob_tx(tx)
+        if bt is None:
+            if pfbs:
+                raise ValueError("normal tx can not be appended after blob tx")
+            normal.append(tx)
+            tx_counter.add(len(tx))
+        else:
+            inner, bl = bt
+            pidx = len(pfbs)
+            pfbs.append([inner, [0] * len(bl)])
+            pfb_counter.add(len(marshal_index_wrapper(inner, [WORST_CASE_SHARE_INDEX] * len(bl))))
+            for bi, b in enumerate(bl):
+                ns = bytes([b["namespace_version"]]) + b["namespace_id"]
+                blobs.append((ns, b["data"], b["share_version"], pidx, bi))
+    blobs.sort(key=lambda e: e[0])               # sort.SliceStable by namespace
+    tx_shares = compact_shares(TX_NS, normal)
+    cursor = tx_counter.size() + pfb_counter.size()
+    non_reserved_start = cursor
+    layout = []
+    for i, (ns, data, ver, pidx, bi) in enumerate(blobs):
+        n = sparse_share_count(len(data))
+        cursor = next_share_index(cursor, n, threshold)
+        if i == 0:
+            non_reserved_start = cursor
+        pfbs[pidx][1][bi] = cursor
+        layout.append((cursor, ns, data, ver))
+        cursor += n
+    pfb_shares = compact_shares(PFB_NS, [marshal_index_wrapper(t, idx) for t, idx in pfbs])
+    total = square_size * square_size
+    square = list(tx_shares) + list(pfb_shares)
+    if layout:
+        square += [padding_share(PRIMARY_RESERVED_PADDING_NS)] * (non_reserved_start - len(square))
+        prev_ns = None
+        for pos, ns, data, ver in layout:
+            if len(square) < pos:
+                square += [padding_share(prev_ns)] * (pos - len(square))
+            square += sparse_shares(ns, data, ver)
+            prev_ns = ns
+    if len(square) > total:
+        raise ValueError("square size too small to fit all blobs")
+    square += [padding_share(TAIL_PADDING_NS)] * (total - len(square))
+    return square
+
+
+def load_block(path: str):
+    d = json.load(open(path))["block"]
+    txs = [base64.b64decode(t) for t in d["data"]["txs"]]
+    k = int(d["data"]["square_size"])
+    data_hash = base64.b64decode(d["header"]["data_hash"])
+    return txs, k, data_hash

@@ -106,3 +106,34 @@ def test_push_order_error(ctx):
     assert (axis, idx, pos) == (0, 2, 6)
     # the EDS itself is still produced (ExtendShares does not check order)
     assert np.array_equal(eds.array().reshape(-1, 512), coracle.extend(ods.reshape(-1, 512)))
+
+
+def test_block408_on_gpu(ctx):
+    """Mainnet block 408 (k=32): GPU data root == header.data_hash."""
+    import gzip, json, os
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(here, "golden", "golden.json")))["block408"]
+    with gzip.open(os.path.join(here, "golden", "block408_ods.bin.gz")) as f:
+        ods = np.frombuffer(f.read(), dtype=np.uint8).reshape(-1, 512).copy()
+    eds = da.extend_shares(ods)
+    dah = da.new_data_availability_header(eds)
+    assert dah.hash().hex() == g["data_hash"]
+    assert hashlib.sha256(eds.array().tobytes()).hexdigest() == g["eds_sha256"]
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32, 64, 128])
+def test_random_fixtures_on_gpu(ctx, k):
+    import json, os
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(here, "golden", "golden.json")))["random_squares"][str(k)]
+    from celestia_da import testfactory
+    ods = testfactory.random_square(k, g["seed_index"])
+    assert hashlib.sha256(ods.tobytes()).hexdigest() == g["ods_sha256"]
+    eds = da.extend_shares(ods)
+    dah = da.new_data_availability_header(eds)
+    assert hashlib.sha256(eds.array().tobytes()).hexdigest() == g["eds_sha256"]
+    rows = np.array([np.frombuffer(r, dtype=np.uint8) for r in dah.row_roots])
+    cols = np.array([np.frombuffer(c, dtype=np.uint8) for c in dah.column_roots])
+    assert hashlib.sha256(rows.tobytes()).hexdigest() == g["row_roots_sha256"]
+    assert hashlib.sha256(cols.tobytes()).hexdigest() == g["col_roots_sha256"]
+    assert dah.hash().hex() == g["data_root"]
