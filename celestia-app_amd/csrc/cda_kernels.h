@@ -24,6 +24,11 @@ struct Gf16Dev {
     const uint16_t* log;   // 65536
     const uint16_t* exp;   // 65536
     const uint16_t* skew;  // 65535
+    // Per-k multiply tables for the register-resident encoder (k = 256, 512):
+    // chunk[idx][16] = 2-bit-chunk v_perm tables of the constant skew[idx]
+    // (all zero when skew[idx] is the modulus, i.e. "multiply by zero").
+    const uint32_t* chunk = nullptr;
+    uint32_t chunk_k = 0;
 };
 hipError_t launch_rs16(const Gf16Dev& t, const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t n_squares,
                        int phase, hipStream_t stream);
@@ -36,8 +41,9 @@ hipError_t launch_order_check(const uint8_t* eds, uint32_t k, uint32_t n_squares
                               hipStream_t stream);
 // err word -> CDA_OK (0) / CDA_ERR_PUSH_ORDER (-3) per square.
 hipError_t launch_status(const uint32_t* err, uint32_t n_squares, int32_t* status, hipStream_t stream);
-// NMT leaf hashing: one 96-B leaf slot per EDS cell, [n][W][W].
-hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n_squares, uint8_t* leaf_slots,
+// NMT leaf hashing: one 96-B leaf slot per EDS cell, [n][W][W]; also runs the
+// Q0 push-order check (same err encoding as launch_order_check).
+hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n_squares, uint8_t* leaf_slots, uint32_t* err,
                          hipStream_t stream);
 // One NMT level for all 2W trees of every square.  `in_leaf` selects the
 // level-0 addressing (row tree t = leaf row t, column tree t = leaf column t);

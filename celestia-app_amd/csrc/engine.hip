@@ -3,10 +3,10 @@
 // Pipeline per batch of n squares of width k (W = 2k), all on one stream:
 //   1. RS phase Q0: rows Q0->Q1 (+ Q0 copy into the EDS) and columns Q0->Q2
 //   2. RS phase Q3: rows Q2->Q3                     (rsmt2d erasureExtendSquare)
-//   3. Q0 namespace push-order check                (nmt Push, ErrInvalidPushOrder)
-//   4. leaf hashing, one per EDS cell               (NmtHasher.HashLeaf)
-//   5. log2(W) NMT levels over all 2W trees         (NmtHasher.HashNode)
-//   6. RFC-6962 data root                           (DataAvailabilityHeader.Hash)
+//   3. leaf hashing, one per EDS cell               (NmtHasher.HashLeaf), fused
+//      with the Q0 namespace push-order check       (nmt Push, ErrInvalidPushOrder)
+//   4. log2(W) NMT levels over all 2W trees         (NmtHasher.HashNode)
+//   5. RFC-6962 data root                           (DataAvailabilityHeader.Hash)
 #include "engine.h"
 
 #include <cstdio>
@@ -44,7 +44,8 @@ Engine::Engine(int device) : device_(device) {}
 
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
-    for (DevBuf* b : {&gf16_log_, &gf16_exp_, &gf16_skew_, &leaf_, &lvl_, &root_slots_, &err_buf_, &h_ods_, &h_eds_,
+    for (DevBuf* b : {&gf16_chunk_[0], &gf16_chunk_[1], &gf16_log_, &gf16_exp_,
+                      &gf16_skew_, &leaf_, &lvl_, &root_slots_, &err_buf_, &h_ods_, &h_eds_,
                       &h_rows_, &h_cols_, &h_roots_})
         b->release();
     for (Mark& m : marks_) {
@@ -83,7 +84,37 @@ int Engine::init() {
     if ((rc = check(hipMemcpy(gf16_exp_.ptr, F->exp, sizeof F->exp, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     if ((rc = check(hipMemcpy(gf16_skew_.ptr, F->skew, sizeof F->skew, hipMemcpyHostToDevice), "hipMemcpy")))
         return rc;
+    // 2-bit-chunk v_perm tables for the constants of the k = 256 / 512 schedules
+    for (int v = 0; v < 2; v++) {
+        const uint32_t k = v == 0 ? 256 : 512, n = 2 * k - 1;
+        std::vector<uint32_t> tab((size_t)n * 16, 0);
+        for (uint32_t idx = 0; idx < n; idx++) {
+            const uint32_t L = F->skew[idx];
+            if (L == LeoField<16>::MOD) continue;    // multiply by zero: all-zero tables
+            for (uint32_t q = 0; q < 8; q++) {
+                const uint32_t shift = q < 4 ? 2 * q : 8 + 2 * (q - 4);
+                for (uint32_t e = 0; e < 4; e++) {
+                    const uint32_t prod = F->mul_log(e << shift, L);
+                    tab[(size_t)idx * 16 + 2 * q] |= (prod & 0xFFu) << (8 * e);
+                    tab[(size_t)idx * 16 + 2 * q + 1] |= (prod >> 8) << (8 * e);
+                }
+            }
+        }
+        if ((rc = check(gf16_chunk_[v].ensure(tab.size() * 4), "hipMalloc"))) return rc;
+        if ((rc = check(hipMemcpy(gf16_chunk_[v].ptr, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "hipMemcpy")))
+            return rc;
+    }
     return CDA_OK;
+}
+
+Gf16Dev Engine::gf16(uint32_t k) const {
+    Gf16Dev t{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
+    if (k == 256 || k == 512) {
+        const int v = k == 256 ? 0 : 1;
+        t.chunk = gf16_chunk_[v].as<uint32_t>();
+        t.chunk_k = k;
+    }
+    return t;
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
@@ -144,7 +175,7 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
         if ((rc = check(launch_rs8(d_ods, d_eds, k, n, kPhaseQ3, s), "rs8 Q3"))) return rc;
         mark_end(s);
     } else {
-        Gf16Dev t{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
+        const Gf16Dev t = gf16(k);
         mark_begin(kStageRsQ0, s);
         if ((rc = check(launch_rs16(t, d_ods, d_eds, k, n, kPhaseQ0, s), "rs16 Q0"))) return rc;
         mark_end(s);
@@ -165,11 +196,8 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     if ((rc = check(lvl_.ensure(slots), "hipMalloc level slots"))) return rc;
     if ((rc = check(root_slots_.ensure((size_t)n * 2 * W * kSlot), "hipMalloc root slots"))) return rc;
     if ((rc = check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync"))) return rc;
-    mark_begin(kStageOrder, s);
-    if ((rc = check(launch_order_check(d_eds, k, n, d_err, s), "order check"))) return rc;
-    mark_end(s);
     mark_begin(kStageLeaves, s);
-    if ((rc = check(launch_leaves(d_eds, k, n, leaf_.as<uint8_t>(), s), "leaf hashing"))) return rc;
+    if ((rc = check(launch_leaves(d_eds, k, n, leaf_.as<uint8_t>(), d_err, s), "leaf hashing"))) return rc;
     mark_end(s);
     mark_begin(kStageLevels, s);
     uint8_t* in = leaf_.as<uint8_t>();

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void order_kernel(const uint8_t* __restrict__ 
 // 0x00 || ns || share, share streamed in 64-B chunks (prefetch one ahead).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void leaf_kernel(const uint8_t* __restrict__ eds, uint32_t k,
-                                                  uint8_t* __restrict__ slots) {
+                                                  uint8_t* __restrict__ slots, uint32_t* __restrict__ err) {
     const uint32_t W = 2 * k;
     const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
     if (cell >= W * W) return;
@@ -146,6 +146,25 @@ __global__ __launch_bounds__(256) void leaf_kernel(const uint8_t* __restrict__ e
     uint32_t out[kSlotWords];
     leaf_node_words(nsw, st.h, out);
     store_slot(slots + (sq * (size_t)W * W + cell) * kSlot, out);
+
+    // nmt push-order check of Q0 (fused: this cell's namespace is in nsw)
+    if (!parity) {
+        uint32_t me[8], nb[8];
+#pragma unroll
+        for (int i = 0; i < 7; i++) me[i] = nsw[i];
+        me[7] = nsw[7] & 0xFF000000u;
+        const uint8_t* E = eds + sq * (size_t)W * W * SH;
+        uint32_t key = 0xFFFFFFFFu;
+        if (c + 1 < k) {
+            load_ns_be(E + ((size_t)r * W + c + 1) * SH, nb);
+            if (ns_less(nb, me)) key = min(key, (0u << 24) | (r << 12) | (c + 1));
+        }
+        if (r + 1 < k) {
+            load_ns_be(E + ((size_t)(r + 1) * W + c) * SH, nb);
+            if (ns_less(nb, me)) key = min(key, (1u << 24) | (c << 12) | (r + 1));
+        }
+        if (key != 0xFFFFFFFFu) atomicMin(err + sq, key);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -272,10 +291,10 @@ hipError_t launch_order_check(const uint8_t* eds, uint32_t k, uint32_t n, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n, uint8_t* slots, hipStream_t s) {
+hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n, uint8_t* slots, uint32_t* err, hipStream_t s) {
     const uint32_t W = 2 * k;
     dim3 grid((W * W + 255) / 256, n);
-    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), 0, s, eds, k, slots);
+    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), 0, s, eds, k, slots, err);
     return hipGetLastError();
 }
 

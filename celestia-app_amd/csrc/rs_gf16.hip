@@ -2,16 +2,32 @@
 //
 // Restates klauspost/reedsolomon v1.12.1 leopardFF16.encode (EXT, pinned at
 // /root/reference/go.mod:152; selected by reedsolomon.New when data+parity
-// shards > 256): same IFFT(coset k)/FFT(coset 0) schedule as GF(2^8); symbol i
-// of every 64-byte block is b[i] | b[i+32] << 8 (lo/hi split layout,
+// shards > 256): the same IFFT(coset k)/FFT(coset 0) schedule as GF(2^8); symbol
+// i of every 64-byte block is b[i] | b[i+32] << 8 (lo/hi split layout,
 // leopard.go refMulAdd).
 //
-// Round-1 kernel: one workgroup per (codeword, 64-byte block column).  The
-// k x 32 symbols of that column are staged in LDS (k = 512 -> 32 KiB) and the
-// 2*log2(k) butterfly layers run in place with a barrier per layer.  Multiply
-// is exp[log[y] + L] with the two 128 KiB tables read through L1/L2 (they stay
-// cache resident).  Correct but gather-bound; the register-resident two-pass
-// encoder is the planned replacement ("next").
+// MI355X mapping (k = 256, 512: rs16_cw_kernel).  One 1024-thread workgroup
+// per codeword (k shards x 512 B).  A lane owns 4 symbols of every shard it
+// holds: the lo dword at byte 64b+4q and the hi dword at 64b+32+4q of the
+// shard (lane = 8b + q), so a wave spans the full 512-B shard width and all
+// its lanes share every butterfly constant (wave-uniform tables in SGPRs).
+//   pass A : wave w holds shards [S*w, S*w+S), S = k/16, and runs the IFFT
+//            layers d < S in registers;
+//   pass B : wave w holds the shards of R = S/16 residues r (r + S*t,
+//            t = 0..15) and runs IFFT d = S..k/2 then FFT d = k/2..S;
+//   pass A': FFT layers d < S, write parity.
+// The two layout changes go through the codeword's own parity region
+// (L2/MALL resident) with a workgroup barrier; no LDS.
+//
+// Multiply by a constant c: y is split into 2-bit chunks (four per byte); each
+// chunk selects one of 4 bytes of a table dword with v_perm_b32(T, T, sel),
+// which needs a single SGPR, so the 16 table dwords of a constant stay in
+// SGPRs: 16 perms + 14 selector ops + 8 XOR3 per 4 symbols.
+//
+// k > 512 (and arbitrary shard lengths in rsmt2d Codec.Encode) use the
+// LDS-staged log/exp kernel rs16_lds_kernel.
+#include <type_traits>
+
 #include "cda_kernels.h"
 
 namespace cda {
@@ -19,7 +35,195 @@ namespace cda {
 namespace {
 
 constexpr uint32_t kMod16 = 65535;
+constexpr size_t SH = 512;
 
+// ---------------------------------------------------------------------------
+// register-resident codeword kernel
+// ---------------------------------------------------------------------------
+struct Chunk16 {   // tables of one constant: t[q][h], q = 2-bit chunk 0..7 of the symbol, h = output byte
+    uint32_t t[16];
+};
+
+__device__ __forceinline__ uint32_t perm1(uint32_t t, uint32_t sel) { return __builtin_amdgcn_perm(t, t, sel); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// (xl, xh) ^= c * (yl, yh) for 4 symbols; tab = 16 dwords of the constant
+// (uniform address -> scalar loads).
+__device__ __forceinline__ void mul_add16(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh,
+                                          const uint32_t* __restrict__ tab) {
+    const uint32_t m = 0x03030303u;
+    const uint32_t l0 = yl & m, l1 = (yl >> 2) & m, l2 = (yl >> 4) & m, l3 = (yl >> 6) & m;
+    const uint32_t h0 = yh & m, h1 = (yh >> 2) & m, h2 = (yh >> 4) & m, h3 = (yh >> 6) & m;
+    // t[2*q + 0] -> lo output byte, t[2*q + 1] -> hi output byte, q: chunks l0..l3 then h0..h3
+    uint32_t a = xor3(perm1(tab[0], l0), perm1(tab[2], l1), perm1(tab[4], l2));
+    uint32_t b = xor3(perm1(tab[6], l3), perm1(tab[8], h0), perm1(tab[10], h1));
+    xl = xor3(xl, a, b);
+    xl = xor3(xl, perm1(tab[12], h2), perm1(tab[14], h3));
+    a = xor3(perm1(tab[1], l0), perm1(tab[3], l1), perm1(tab[5], l2));
+    b = xor3(perm1(tab[7], l3), perm1(tab[9], h0), perm1(tab[11], h1));
+    xh = xor3(xh, a, b);
+    xh = xor3(xh, perm1(tab[13], h2), perm1(tab[15], h3));
+}
+
+// tab layout: [skew index][16 dwords].  A skew equal to the modulus means
+// "multiply by zero" (leopard skips the multiply); its tables are all zero, so
+// the butterfly stays branch-free and bit-identical.
+struct Tab16 {
+    const uint32_t* __restrict__ t;      // [2k-1][16]
+};
+
+__device__ __forceinline__ void ifft_bfly(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const Tab16& T,
+                                          uint32_t idx) {
+    yl ^= xl;
+    yh ^= xh;
+    mul_add16(xl, xh, yl, yh, T.t + (size_t)idx * 16);
+}
+__device__ __forceinline__ void fft_bfly(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const Tab16& T,
+                                         uint32_t idx) {
+    mul_add16(xl, xh, yl, yh, T.t + (size_t)idx * 16);
+    yl ^= xl;
+    yh ^= xh;
+}
+
+// Compile-time loops (full unroll with constant register indices: no
+// s_set_gpr_idx register indexing, no scratch).
+template <int B, int E, int STEP, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + STEP, E, STEP>(f);
+    }
+}
+
+// In-register IFFT / FFT layers over N consecutive registers holding shards
+// base + i*stride_abs; constant index of group g (register space) is
+// IDX(g, d) (uniform).
+template <int N, class IdxF>
+__device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
+    sfor<0, 8, 1>([&](auto ld) {
+        constexpr int d = 1 << decltype(ld)::value;
+        if constexpr (d < N) {
+            sfor<0, N, 2 * d>([&](auto gg) {
+                constexpr int g = decltype(gg)::value;
+                const uint32_t idx = idxf(g, d);
+                asm volatile("" ::: "memory");   // one constant's tables in SGPRs at a time
+                sfor<g, g + d, 1>([&](auto ii) {
+                    constexpr int i = decltype(ii)::value;
+                    ifft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
+                });
+            });
+        }
+    });
+}
+template <int N, class IdxF>
+__device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
+    sfor<0, 8, 1>([&](auto ld) {
+        constexpr int d = (N / 2) >> decltype(ld)::value;
+        if constexpr (d >= 1) {
+            sfor<0, N, 2 * d>([&](auto gg) {
+                constexpr int g = decltype(gg)::value;
+                const uint32_t idx = idxf(g, d);
+                asm volatile("" ::: "memory");
+                sfor<g, g + d, 1>([&](auto ii) {
+                    constexpr int i = decltype(ii)::value;
+                    fft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
+                });
+            });
+        }
+    });
+}
+
+template <int K>
+__global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const uint8_t* __restrict__ ods,
+                                                      uint8_t* __restrict__ eds, int phase) {
+    constexpr int S = K / 16;      // shards per lane in pass A
+    constexpr int R = S / 16;      // residues per wave in pass B
+    constexpr uint32_t W = 2 * K;
+    const Tab16 T{tab};
+    const uint32_t cw = blockIdx.x;
+    const size_t sq = blockIdx.y;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t off = 64 * (lane >> 3) + 4 * (lane & 7);    // lo dword; hi at +32
+    // All addressing is a uniform base pointer + a 32-bit byte offset (one
+    // VGPR per access, saddr form), so no 64-bit address pairs stay live.
+    const uint8_t* src_base;
+    uint32_t s0, ss;                    // source: shard i at src_base + s0 + i*ss
+    uint8_t* E = eds + sq * (size_t)W * W * SH;
+    uint32_t d0, ds;                    // parity / scratch: shard i at E + d0 + i*ds
+    uint32_t c0 = 0xFFFFFFFFu;          // Q0 copy: shard i at E + c0 + i*SH
+    if (phase == kPhaseQ0) {
+        src_base = ods + sq * (size_t)K * K * SH;
+        if (cw < K) {
+            s0 = cw * K * (uint32_t)SH; ss = SH;
+            d0 = (cw * W + K) * (uint32_t)SH; ds = SH;
+            c0 = cw * W * (uint32_t)SH;
+        } else {
+            const uint32_t j = cw - K;
+            s0 = j * (uint32_t)SH; ss = K * (uint32_t)SH;
+            d0 = (K * W + j) * (uint32_t)SH; ds = W * (uint32_t)SH;
+        }
+    } else {
+        src_base = E;
+        s0 = (K + cw) * W * (uint32_t)SH; ss = SH;
+        d0 = ((K + cw) * W + K) * (uint32_t)SH; ds = SH;
+    }
+    // `lo_off` is re-laundered at every use site so the compiler recomputes
+    // (one v_add) instead of keeping dozens of per-shard addresses live.
+    auto lane_off = [&]() {
+        uint32_t o = off;
+        asm volatile("" : "+v"(o));
+        return o;
+    };
+    auto ld = [&](const uint8_t* base, uint32_t o, uint32_t& l, uint32_t& h) {
+        const uint32_t a = o + lane_off();
+        l = *reinterpret_cast<const uint32_t*>(base + a);
+        h = *reinterpret_cast<const uint32_t*>(base + a + 32);
+    };
+    auto st = [&](uint8_t* base, uint32_t o, uint32_t l, uint32_t h) {
+        const uint32_t a = o + lane_off();
+        *reinterpret_cast<uint32_t*>(base + a) = l;
+        *reinterpret_cast<uint32_t*>(base + a + 32) = h;
+    };
+
+    // ---------------- pass A: IFFT d = 1 .. S/2 -------------------------
+    {
+        uint32_t lo[S], hi[S];
+        const uint32_t base = S * wave;
+        sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (base + jj.value) * ss, lo[jj.value], hi[jj.value]); });
+        if (c0 != 0xFFFFFFFFu) {
+            sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * (uint32_t)SH, lo[jj.value], hi[jj.value]); });
+        }
+        ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + base; });
+        sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
+    }
+    __syncthreads();
+    // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
+    sfor<0, R, 1>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        uint32_t lo[16], hi[16];
+        const uint32_t b0 = d0 + (R * wave + r) * ds;
+        sfor<0, 16, 1>([&](auto tt) { ld(E, b0 + (S * tt.value) * ds, lo[tt.value], hi[tt.value]); });
+        ifft_regs<16>(lo, hi, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
+        fft_regs<16>(lo, hi, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
+        sfor<0, 16, 1>([&](auto tt) { st(E, b0 + (S * tt.value) * ds, lo[tt.value], hi[tt.value]); });
+    });
+    __syncthreads();
+    // ---------------- pass A': FFT d = S/2 .. 1 --------------------------
+    {
+        uint32_t lo[S], hi[S];
+        const uint32_t base = S * wave;
+        sfor<0, S, 1>([&](auto jj) { ld(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
+        fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + base; });
+        sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-staged log/exp kernel (any k with k*64 B of LDS, any shard length)
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t mul16(const uint16_t* __restrict__ lg, const uint16_t* __restrict__ ex, uint32_t y,
                                           uint32_t L) {
     if (y == 0) return 0;
@@ -32,12 +236,10 @@ __device__ __forceinline__ uint32_t mul16(const uint16_t* __restrict__ lg, const
 __device__ void encode_block_column(const Gf16Dev& t, uint16_t* sym, uint32_t k, const uint8_t* src, size_t src_stride,
                                     uint8_t* dst, size_t dst_stride, uint8_t* copy, size_t copy_stride) {
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    // load: thread handles (shard i, word q) -- 16 words of 4 bytes per shard block
     for (uint32_t w = tid; w < k * 16; w += nt) {
         const uint32_t i = w >> 4, q = w & 15;
         const uint32_t v = reinterpret_cast<const uint32_t*>(src + i * src_stride)[q];
         if (copy) reinterpret_cast<uint32_t*>(copy + i * copy_stride)[q] = v;
-        // bytes 4q..4q+3 of the block: lo bytes for q < 8, hi bytes for q >= 8
         uint8_t* s8 = reinterpret_cast<uint8_t*>(sym + i * 32);
         const uint32_t base = (q & 7) * 4;
         const uint32_t hi = q >> 3;
@@ -47,7 +249,7 @@ __device__ void encode_block_column(const Gf16Dev& t, uint16_t* sym, uint32_t k,
     __syncthreads();
     const uint32_t m = k;
     const uint32_t items = (m / 2) * 32;
-    for (uint32_t d = 1; d < m; d <<= 1) {       // IFFT (ifftDITEncoder)
+    for (uint32_t d = 1; d < m; d <<= 1) {
         for (uint32_t w = tid; w < items; w += nt) {
             const uint32_t p = w >> 5, s = w & 31;
             const uint32_t g = (p / d) * 2 * d, i = g + (p % d);
@@ -60,7 +262,7 @@ __device__ void encode_block_column(const Gf16Dev& t, uint16_t* sym, uint32_t k,
         }
         __syncthreads();
     }
-    for (uint32_t d = m >> 1; d >= 1; d >>= 1) {  // FFT (fftDIT)
+    for (uint32_t d = m >> 1; d >= 1; d >>= 1) {
         for (uint32_t w = tid; w < items; w += nt) {
             const uint32_t p = w >> 5, s = w & 31;
             const uint32_t g = (p / d) * 2 * d, i = g + (p % d);
@@ -84,12 +286,11 @@ __device__ void encode_block_column(const Gf16Dev& t, uint16_t* sym, uint32_t k,
     }
 }
 
-__global__ __launch_bounds__(256) void rs16_square_kernel(Gf16Dev t, const uint8_t* __restrict__ ods,
-                                                         uint8_t* __restrict__ eds, uint32_t k, int phase) {
+__global__ __launch_bounds__(256) void rs16_lds_kernel(Gf16Dev t, const uint8_t* __restrict__ ods,
+                                                      uint8_t* __restrict__ eds, uint32_t k, int phase) {
     extern __shared__ __attribute__((aligned(16))) uint16_t sym[];
-    constexpr size_t SH = 512;
     const uint32_t W = 2 * k;
-    const uint32_t cw = blockIdx.x >> 3;       // 8 blocks of 64 B per share
+    const uint32_t cw = blockIdx.x >> 3;
     const uint32_t blk = blockIdx.x & 7;
     const size_t sq = blockIdx.y;
     const uint8_t* O = ods + sq * (size_t)k * k * SH;
@@ -119,15 +320,26 @@ __global__ __launch_bounds__(256) void rs16_flat_kernel(Gf16Dev t, const uint8_t
                         nullptr, 0);
 }
 
+template <int K>
+hipError_t launch_cw(const Gf16Dev& t, const uint8_t* ods, uint8_t* eds, uint32_t n, int phase, hipStream_t s) {
+    dim3 grid(phase == kPhaseQ0 ? 2 * K : K, n);
+    hipLaunchKernelGGL(rs16_cw_kernel<K>, grid, dim3(1024), 0, s, t.chunk, ods, eds, phase);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_rs16(const Gf16Dev& t, const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t n, int phase,
                        hipStream_t s) {
     if (k < 2 || (k & (k - 1)) || k > 32768) return hipErrorInvalidValue;
+    if (t.chunk && t.chunk_k == k) {
+        if (k == 256) return launch_cw<256>(t, ods, eds, n, phase, s);
+        if (k == 512) return launch_cw<512>(t, ods, eds, n, phase, s);
+    }
     const size_t lds = (size_t)k * 64;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
     dim3 grid((phase == kPhaseQ0 ? 2 * k : k) * 8, n);
-    hipLaunchKernelGGL(rs16_square_kernel, grid, dim3(256), lds, s, t, ods, eds, k, phase);
+    hipLaunchKernelGGL(rs16_lds_kernel, grid, dim3(256), lds, s, t, ods, eds, k, phase);
     return hipGetLastError();
 }
 
@@ -135,7 +347,7 @@ hipError_t launch_rs16_flat(const Gf16Dev& t, const uint8_t* d, uint8_t* p, uint
                             hipStream_t s) {
     if (k < 2 || (k & (k - 1)) || len % 64) return hipErrorInvalidValue;
     const size_t lds = (size_t)k * 64;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
     dim3 grid(len / 64, n);
     hipLaunchKernelGGL(rs16_flat_kernel, grid, dim3(256), lds, s, t, d, p, k, len);
     return hipGetLastError();

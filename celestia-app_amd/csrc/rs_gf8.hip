@@ -15,9 +15,9 @@
 // wave-instruction (share-major streaming).  Column codewords use the same
 // code with a k*512-B shard stride (a strided gather, no physical transpose).
 //
-// GF(2^8) multiply by a constant c: two 16-entry nibble tables evaluated with
-// four v_perm_b32 (leopard_tables.h solve_nibble_perm) -- 11 VALU ops per
-// 4 bytes, tables folded to immediates.
+// GF(2^8) multiply by a constant c: the byte is cut into four 2-bit chunks,
+// each looked up in a 4-entry table dword with v_perm_b32(T, T, sel) -- 4 perms
+// (half rate), 7 selector ops, 2 XOR3 per 4 bytes; tables are immediates.
 #include "cda_kernels.h"
 #include "leopard_tables.h"
 
@@ -27,12 +27,20 @@ namespace {
 
 constexpr LeoField<8> kF8 = make_gf8();
 
+// 2-bit-chunk tables: c[q] byte e = mul_log(e << 2q, L).  v_perm_b32(T, T, sel)
+// with sel bytes in 0..3 reads byte sel of T and needs one SGPR operand, so the
+// four table dwords are scalar immediates (s_mov) -- no VGPR materialisation.
+struct Mul8Chunks {
+    uint32_t c[4];
+};
 struct Mul8All {
-    Mul8Perm t[256];
+    Mul8Chunks t[256];
 };
 constexpr Mul8All make_all_mul8() {
     Mul8All a{};
-    for (uint32_t l = 0; l < 256; l++) a.t[l] = make_mul8_perm(kF8, l);
+    for (uint32_t l = 0; l < 256; l++)
+        for (uint32_t q = 0; q < 4; q++)
+            for (uint32_t e = 0; e < 4; e++) a.t[l].c[q] |= (uint32_t)kF8.mul_log(e << (2 * q), l) << (8 * e);
     return a;
 }
 constexpr Mul8All kMul8 = make_all_mul8();
@@ -42,15 +50,21 @@ __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
     return __builtin_amdgcn_perm(s0, s1, sel);
 }
 
-// x ^ c*y for the compile-time constant with log L.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// x ^ c*y for the compile-time constant with log L (4 perms, 7 selector ops,
+// 2 XOR3).
 template <uint32_t L>
 __device__ __forceinline__ uint32_t mul_add(uint32_t x, uint32_t y) {
-    constexpr Mul8Perm T = kMul8.t[L];
-    const uint32_t lo = y & 0x0F0F0F0Fu;
-    const uint32_t hi = (y >> 4) & 0x0F0F0F0Fu;
-    const uint32_t r0 = perm(T.lo.a_hi, T.lo.a_lo, lo) ^ perm(T.lo.b_hi, T.lo.b_lo, lo ^ 0x08080808u);
-    const uint32_t r1 = perm(T.hi.a_hi, T.hi.a_lo, hi) ^ perm(T.hi.b_hi, T.hi.b_lo, hi ^ 0x08080808u);
-    return x ^ r0 ^ r1;
+    constexpr Mul8Chunks T = kMul8.t[L];
+    constexpr uint32_t m = 0x03030303u;
+    const uint32_t p0 = perm(T.c[0], T.c[0], y & m);
+    const uint32_t p1 = perm(T.c[1], T.c[1], (y >> 2) & m);
+    const uint32_t p2 = perm(T.c[2], T.c[2], (y >> 4) & m);
+    const uint32_t p3 = perm(T.c[3], T.c[3], (y >> 6) & m);
+    return xor3(x, xor3(p0, p1, p2), p3);
 }
 
 template <int M, int D, int G>
@@ -113,7 +127,7 @@ __device__ __forceinline__ void encode_regs(uint32_t (&v)[M]) {
 // Register budget: K data VGPRs + temporaries; ask for >= 2 waves per SIMD so
 // the VALU issue of one wave hides behind its partner's.
 template <int K>
-constexpr int waves_per_simd() { return K >= 128 ? 2 : K >= 64 ? 3 : 4; }
+constexpr int waves_per_simd() { return K >= 128 ? 2 : 4; }
 
 template <int K>
 __global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_square_kernel(const uint8_t* __restrict__ ods, uint8_t* __restrict__ eds,
