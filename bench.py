@@ -65,9 +65,10 @@ def stage_report(st: dict, k: int, batch: int) -> dict:
 
 def load_traffic(stage: str):
     """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary
-    (profiles/pmc_*.json, written by tools/pmc_summary.py), else None."""
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), else None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
         return None
     try:

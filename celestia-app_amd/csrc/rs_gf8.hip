@@ -136,44 +136,41 @@ __global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_square_kernel(co
     constexpr size_t SH = 512;
     const uint32_t cw = blockIdx.x;
     const size_t sq = blockIdx.y;
-    const uint32_t lane = threadIdx.x;  // 0..127 -> byte offset 4*lane
-    const uint8_t* src;
-    size_t src_stride;
-    uint8_t* dst;
-    size_t dst_stride;
-    uint8_t* copy = nullptr;
+    // Uniform base pointer + 32-bit byte offsets (saddr addressing).
+    const uint32_t lane4 = threadIdx.x * 4;   // byte offset inside the 512-B shard
+    auto lane_off = [&]() { return lane4; };
     const uint8_t* O = ods + sq * (size_t)K * K * SH;
     uint8_t* E = eds + sq * (size_t)W * W * SH;
+    const uint8_t* src_base;
+    uint32_t s0, ss, d0, ds;
+    uint32_t c0 = 0xFFFFFFFFu;
     if (phase == kPhaseQ0) {
-        if (cw < K) {  // row cw: Q0 -> Q1
-            src = O + (size_t)cw * K * SH;
-            src_stride = SH;
-            dst = E + ((size_t)cw * W + K) * SH;
-            dst_stride = SH;
-            copy = E + (size_t)cw * W * SH;
+        src_base = O;
+        if (cw < K) {  // row cw: Q0 -> Q1 (and copy Q0 into the EDS)
+            s0 = cw * K * (uint32_t)SH; ss = SH;
+            d0 = (cw * W + K) * (uint32_t)SH; ds = SH;
+            c0 = cw * W * (uint32_t)SH;
         } else {  // column j: Q0 -> Q2
             const uint32_t j = cw - K;
-            src = O + (size_t)j * SH;
-            src_stride = (size_t)K * SH;
-            dst = E + ((size_t)K * W + j) * SH;
-            dst_stride = (size_t)W * SH;
+            s0 = j * (uint32_t)SH; ss = K * (uint32_t)SH;
+            d0 = (K * W + j) * (uint32_t)SH; ds = W * (uint32_t)SH;
         }
     } else {  // row K+cw: Q2 -> Q3
-        src = E + (size_t)(K + cw) * W * SH;
-        src_stride = SH;
-        dst = E + ((size_t)(K + cw) * W + K) * SH;
-        dst_stride = SH;
+        src_base = E;
+        s0 = (K + cw) * W * (uint32_t)SH; ss = SH;
+        d0 = ((K + cw) * W + K) * (uint32_t)SH; ds = SH;
     }
     uint32_t v[K];
 #pragma unroll
-    for (int i = 0; i < K; i++) v[i] = reinterpret_cast<const uint32_t*>(src + i * src_stride)[lane];
-    if (copy) {
+    for (int i = 0; i < K; i++)
+        v[i] = *reinterpret_cast<const uint32_t*>(src_base + (s0 + i * ss + lane_off()));
+    if (c0 != 0xFFFFFFFFu) {
 #pragma unroll
-        for (int i = 0; i < K; i++) reinterpret_cast<uint32_t*>(copy + i * SH)[lane] = v[i];
+        for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(E + (c0 + i * (uint32_t)SH + lane_off())) = v[i];
     }
     encode_regs<K>(v);
 #pragma unroll
-    for (int i = 0; i < K; i++) reinterpret_cast<uint32_t*>(dst + i * dst_stride)[lane] = v[i];
+    for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(E + (d0 + i * ds + lane_off())) = v[i];
 }
 
 // Flat codewords: codeword c = data[c*K*len ...], shards of len bytes.
