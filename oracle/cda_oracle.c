@@ -69,6 +69,71 @@ static void sha256_block(uint32_t st[8], const uint8_t *p) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+/* SHA-NI compression (x86 SHA extensions), used by the CPU-baseline path when
+ * the host supports it -- Go's crypto/sha256 does the same on amd64.  Tested
+ * bit-equal to sha256_block (tests/test_oracle.py). */
+#if defined(__x86_64__)
+#include <immintrin.h>
+__attribute__((target("sha,sse4.1,ssse3"))) static void sha256_block_ni(uint32_t st[8], const uint8_t *p) {
+    const __m128i MASK = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i TMP = _mm_loadu_si128((const __m128i *)&st[0]);
+    __m128i STATE1 = _mm_loadu_si128((const __m128i *)&st[4]);
+    TMP = _mm_shuffle_epi32(TMP, 0xB1);          /* CDAB */
+    STATE1 = _mm_shuffle_epi32(STATE1, 0x1B);    /* EFGH */
+    __m128i STATE0 = _mm_alignr_epi8(TMP, STATE1, 8);   /* ABEF */
+    STATE1 = _mm_blend_epi16(STATE1, TMP, 0xF0);        /* CDGH */
+    const __m128i ABEF_SAVE = STATE0, CDGH_SAVE = STATE1;
+    __m128i MSG, MSG0, MSG1, MSG2, MSG3;
+    MSG0 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 0)), MASK);
+    MSG1 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 16)), MASK);
+    MSG2 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 32)), MASK);
+    MSG3 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(p + 48)), MASK);
+    __m128i W[4] = {MSG0, MSG1, MSG2, MSG3};
+    for (int r = 0; r < 16; r++) {
+        __m128i k = _mm_loadu_si128((const __m128i *)&K256[4 * r]);
+        MSG = _mm_add_epi32(W[r & 3], k);
+        STATE1 = _mm_sha256rnds2_epu32(STATE1, STATE0, MSG);
+        MSG = _mm_shuffle_epi32(MSG, 0x0E);
+        STATE0 = _mm_sha256rnds2_epu32(STATE0, STATE1, MSG);
+        if (r < 12) {
+            /* W[r+4] = msg2(msg1(W[r], W[r+1]) + alignr(W[r+3], W[r+2]), W[r+3]) */
+            __m128i t = _mm_sha256msg1_epu32(W[r & 3], W[(r + 1) & 3]);
+            t = _mm_add_epi32(t, _mm_alignr_epi8(W[(r + 3) & 3], W[(r + 2) & 3], 4));
+            W[r & 3] = _mm_sha256msg2_epu32(t, W[(r + 3) & 3]);
+        }
+    }
+    STATE0 = _mm_add_epi32(STATE0, ABEF_SAVE);
+    STATE1 = _mm_add_epi32(STATE1, CDGH_SAVE);
+    TMP = _mm_shuffle_epi32(STATE0, 0x1B);       /* FEBA */
+    STATE1 = _mm_shuffle_epi32(STATE1, 0xB1);    /* DCHG */
+    STATE0 = _mm_blend_epi16(TMP, STATE1, 0xF0); /* DCBA */
+    STATE1 = _mm_alignr_epi8(STATE1, TMP, 8);    /* ABEF */
+    _mm_storeu_si128((__m128i *)&st[0], STATE0);
+    _mm_storeu_si128((__m128i *)&st[4], STATE1);
+}
+static int have_sha_ni(void) {
+    static int v = -1;
+    if (v < 0) v = __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+    return v;
+}
+#else
+static void sha256_block_ni(uint32_t st[8], const uint8_t *p) { sha256_block(st, p); }
+static int have_sha_ni(void) { return 0; }
+#endif
+
+/* 0 = portable scalar (the checker), 1 = SHA-NI when available (baseline). */
+static __thread int g_fast = 0;
+static void sha_block_dispatch(uint32_t st[8], const uint8_t *p) {
+    if (g_fast && have_sha_ni()) sha256_block_ni(st, p);
+    else sha256_block(st, p);
+}
+
+void oracle_sha256_block_test(uint32_t st[8], const uint8_t *p, int ni) {
+    if (ni && have_sha_ni()) sha256_block_ni(st, p);
+    else sha256_block(st, p);
+}
+int oracle_have_sha_ni(void) { return have_sha_ni(); }
+
 typedef struct { uint32_t st[8]; uint8_t buf[64]; uint64_t len; } sha_ctx;
 
 static void sha_init(sha_ctx *c) {
@@ -83,7 +148,7 @@ static void sha_update(sha_ctx *c, const uint8_t *p, size_t n) {
         if (take > n) take = n;
         memcpy(c->buf + off, p, take);
         c->len += take; p += take; n -= take;
-        if ((c->len & 63) == 0) sha256_block(c->st, c->buf);
+        if ((c->len & 63) == 0) sha_block_dispatch(c->st, c->buf);
     }
 }
 static void sha_final(sha_ctx *c, uint8_t out[32]) {
@@ -201,6 +266,95 @@ static void encode_symbols(const field *F, uint16_t *w, uint32_t m, size_t lanes
         }
 }
 
+/* ------------------------------------------------------------------ */
+/* CPU-baseline RS: same butterflies, multiply with PSHUFB nibble tables */
+/* (the klauspost/reedsolomon amd64 technique: mulAdd via VPSHUFB).     */
+/* Used only by oracle_cpu_baseline; tested bit-equal to the scalar path. */
+/* ------------------------------------------------------------------ */
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) static void mul_add8_avx2(uint8_t *x, const uint8_t *y, size_t n, const field *F,
+                                                           uint32_t L) {
+    uint8_t tl[16], th[16];
+    for (int i = 0; i < 16; i++) { tl[i] = (uint8_t)mul_log(F, i, L); th[i] = (uint8_t)mul_log(F, i << 4, L); }
+    const __m256i TL = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)tl));
+    const __m256i TH = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)th));
+    const __m256i M = _mm256_set1_epi8(0x0F);
+    size_t i = 0;
+    for (; i + 32 <= n; i += 32) {
+        __m256i v = _mm256_loadu_si256((const __m256i *)(y + i));
+        __m256i lo = _mm256_and_si256(v, M), hi = _mm256_and_si256(_mm256_srli_epi64(v, 4), M);
+        __m256i p = _mm256_xor_si256(_mm256_shuffle_epi8(TL, lo), _mm256_shuffle_epi8(TH, hi));
+        _mm256_storeu_si256((__m256i *)(x + i), _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(x + i)), p));
+    }
+    for (; i < n; i++) x[i] ^= (uint8_t)mul_log(F, y[i], L);
+}
+/* GF(2^16), lo/hi split layout: per 64-byte block b[0..31] lo, b[32..63] hi. */
+__attribute__((target("avx2"))) static void mul_add16_avx2(uint8_t *x, const uint8_t *y, size_t n, const field *F,
+                                                            uint32_t L) {
+    uint8_t t[8][16];   /* [nibble q][lo/hi out][16] */
+    for (int q = 0; q < 4; q++)
+        for (int v = 0; v < 16; v++) {
+            uint32_t pr = mul_log(F, (uint32_t)v << (4 * q), L);
+            t[2 * q][v] = (uint8_t)pr;
+            t[2 * q + 1][v] = (uint8_t)(pr >> 8);
+        }
+    __m256i T[8];
+    for (int i = 0; i < 8; i++) T[i] = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)t[i]));
+    const __m256i M = _mm256_set1_epi8(0x0F);
+    for (size_t i = 0; i + 64 <= n; i += 64) {
+        __m256i lo = _mm256_loadu_si256((const __m256i *)(y + i)), hi = _mm256_loadu_si256((const __m256i *)(y + i + 32));
+        __m256i n0 = _mm256_and_si256(lo, M), n1 = _mm256_and_si256(_mm256_srli_epi64(lo, 4), M);
+        __m256i n2 = _mm256_and_si256(hi, M), n3 = _mm256_and_si256(_mm256_srli_epi64(hi, 4), M);
+        __m256i pl = _mm256_xor_si256(_mm256_xor_si256(_mm256_shuffle_epi8(T[0], n0), _mm256_shuffle_epi8(T[2], n1)),
+                                      _mm256_xor_si256(_mm256_shuffle_epi8(T[4], n2), _mm256_shuffle_epi8(T[6], n3)));
+        __m256i ph = _mm256_xor_si256(_mm256_xor_si256(_mm256_shuffle_epi8(T[1], n0), _mm256_shuffle_epi8(T[3], n1)),
+                                      _mm256_xor_si256(_mm256_shuffle_epi8(T[5], n2), _mm256_shuffle_epi8(T[7], n3)));
+        _mm256_storeu_si256((__m256i *)(x + i), _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(x + i)), pl));
+        _mm256_storeu_si256((__m256i *)(x + i + 32),
+                            _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(x + i + 32)), ph));
+    }
+}
+__attribute__((target("avx2"))) static void xor_avx2(uint8_t *y, const uint8_t *x, size_t n) {
+    size_t i = 0;
+    for (; i + 32 <= n; i += 32)
+        _mm256_storeu_si256((__m256i *)(y + i), _mm256_xor_si256(_mm256_loadu_si256((const __m256i *)(y + i)),
+                                                                  _mm256_loadu_si256((const __m256i *)(x + i))));
+    for (; i < n; i++) y[i] ^= x[i];
+}
+static int have_avx2(void) {
+    static int v = -1;
+    if (v < 0) v = __builtin_cpu_supports("avx2");
+    return v;
+}
+#else
+static int have_avx2(void) { return 0; }
+static void mul_add8_avx2(uint8_t *x, const uint8_t *y, size_t n, const field *F, uint32_t L) {}
+static void mul_add16_avx2(uint8_t *x, const uint8_t *y, size_t n, const field *F, uint32_t L) {}
+static void xor_avx2(uint8_t *y, const uint8_t *x, size_t n) {}
+#endif
+
+/* Leopard encode on byte shards w[i] (len bytes each), in place: w[0..k) data
+ * -> parity.  Same layer order as encode_symbols. */
+static void encode_bytes_fast(const field *F, uint8_t **w, uint32_t m, size_t len) {
+    const int f16 = F->bits == 16;
+    for (uint32_t d = 1; d < m; d <<= 1)
+        for (uint32_t g = 0; g < m; g += 2 * d) {
+            uint32_t L = F->skew[m - 1 + g + d];
+            for (uint32_t i = g; i < g + d; i++) {
+                xor_avx2(w[i + d], w[i], len);
+                if (L != F->mod) (f16 ? mul_add16_avx2 : mul_add8_avx2)(w[i], w[i + d], len, F, L);
+            }
+        }
+    for (uint32_t d = m >> 1; d >= 1; d >>= 1)
+        for (uint32_t g = 0; g < m; g += 2 * d) {
+            uint32_t L = F->skew[g + d - 1];
+            for (uint32_t i = g; i < g + d; i++) {
+                if (L != F->mod) (f16 ? mul_add16_avx2 : mul_add8_avx2)(w[i], w[i + d], len, F, L);
+                xor_avx2(w[i + d], w[i], len);
+            }
+        }
+}
+
 /* LeoRSCodec.Encode on k shards of `len` bytes given as pointers (strided
  * access lets the caller encode a column in place).  Returns 0 or -2 for a
  * chunk size that is not a multiple of 64. */
@@ -209,6 +363,13 @@ int oracle_leopard_encode_ptrs(const uint8_t *const *data, uint8_t *const *parit
     if (len % 64) return -2;
     if (k == 1) { memcpy(parity[0], data[0], len); return 0; }
     const field *F = (2 * k <= 256) ? &F8 : &F16;
+    if (g_fast && have_avx2()) {     /* CPU-baseline path: work in place in the parity shards */
+        uint8_t **w = malloc(k * sizeof *w);
+        for (uint32_t i = 0; i < k; i++) { memcpy(parity[i], data[i], len); w[i] = parity[i]; }
+        encode_bytes_fast(F, w, k, len);
+        free(w);
+        return 0;
+    }
     if (F->bits == 8) {
         uint16_t *w = malloc((size_t)k * len * 2);
         for (uint32_t i = 0; i < k; i++)
@@ -425,6 +586,7 @@ typedef struct {
 
 static void *worker(void *arg) {
     job *j = arg;
+    g_fast = 1;   /* SHA-NI + AVX2 nibble-table RS, like Go's amd64 assembly */
     uint32_t W = 2 * j->k;
     for (;;) {
         pthread_mutex_lock(&j->mu);
@@ -455,6 +617,9 @@ static void run_phase(job *j, int phase, int nthreads) {
 
 int oracle_cpu_baseline(const uint8_t *ods, uint32_t k, uint8_t *eds, uint8_t *rows, uint8_t *cols,
                         uint8_t root[32], int nthreads) {
+    if (nthreads == 0) {   /* scalar single-thread path through the same scheduler (tests) */
+        return oracle_extend_dah(ods, k, eds, rows, cols, root);
+    }
     pthread_once(&fields_once, fields_init);
     if (k == 0 || (k & (k - 1))) return -1;
     if (nthreads < 1) nthreads = 1;

@@ -142,11 +142,29 @@ def test_gf16_codec_c_matches_python():
     assert np.array_equal(coracle.leopard_encode(data), pyref.leopard_encode(data))
 
 
-def test_cpu_baseline_equals_scalar_oracle():
-    ods = coracle.random_square(16, 3)
+@pytest.mark.parametrize("k", [16, 64, 256])
+def test_cpu_baseline_equals_scalar_oracle(k):
+    """The baseline path (SHA-NI + AVX2 nibble-table RS, threads) is bit-equal
+    to the scalar checker, GF(2^8) and GF(2^16)."""
+    ods = coracle.random_square(k, 3)
     a = coracle.extend_dah(ods)
     b = coracle.cpu_baseline(ods, 4)
     assert np.array_equal(a[0], b[0]) and a[3] == b[3]
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+
+
+def test_sha_ni_block_matches_portable():
+    import ctypes as C
+    L = coracle.lib()
+    L.oracle_sha256_block_test.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint8), C.c_int]
+    rng = np.random.default_rng(1)
+    for _ in range(64):
+        blk = rng.integers(0, 256, 64, dtype=np.uint8)
+        st = rng.integers(0, 2**32, 8, dtype=np.uint64).astype(np.uint32)
+        a, b = st.copy(), st.copy()
+        L.oracle_sha256_block_test(a.ctypes.data_as(C.POINTER(C.c_uint32)), blk.ctypes.data_as(C.POINTER(C.c_uint8)), 0)
+        L.oracle_sha256_block_test(b.ctypes.data_as(C.POINTER(C.c_uint32)), blk.ctypes.data_as(C.POINTER(C.c_uint8)), 1)
+        assert np.array_equal(a, b)
 
 
 def test_push_order_detected_by_oracle():
