@@ -32,6 +32,7 @@ EXPORTED = (
     "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
     "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
     "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
+    "cda_split_rows", "cda_split_cols", "cda_split_combine",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -78,6 +79,9 @@ def load():
         L.cda_data_root.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p]
         L.cda_push_order_detail.argtypes = [ctxp, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
                                             C.POINTER(C.c_uint32)]
+        L.cda_split_rows.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
+        L.cda_split_cols.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+        L.cda_split_combine.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L
@@ -136,6 +140,17 @@ class Context:
         """Enqueue the whole path on device pointers (asynchronous)."""
         self.check(self.lib.cda_extend_dah_device(self.h, d_ods, k, n, d_eds, d_rows, d_cols, d_roots,
                                                   d_status, stream))
+
+    # -- config 5 (one square split across ranks); device pointers as ints --
+    def split_rows(self, d_rows, k, n_rows, row0, d_block, d_err, stream=None):
+        self.check(self.lib.cda_split_rows(self.h, d_rows, k, n_rows, row0, d_block, d_err, stream))
+
+    def split_cols(self, d_block, k, n_cols, col0, d_col_slots, d_row_sub, d_err, stream=None):
+        self.check(self.lib.cda_split_cols(self.h, d_block, k, n_cols, col0, d_col_slots, d_row_sub, d_err, stream))
+
+    def split_combine(self, d_row_sub, parts, k, d_col_slots, d_rows, d_cols, d_root, stream=None):
+        self.check(self.lib.cda_split_combine(self.h, d_row_sub, parts, k, d_col_slots, d_rows, d_cols, d_root,
+                                              stream))
 
     def push_order_detail(self):
         a, i, p = C.c_int32(), C.c_uint32(), C.c_uint32()

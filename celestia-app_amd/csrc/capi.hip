@@ -161,6 +161,42 @@ int cda_push_order_detail(cda_ctx* ctx, int32_t* axis, uint32_t* index, uint32_t
     return CDA_OK;
 }
 
+int cda_split_rows(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
+                   void* d_row_block, uint32_t* d_err, void* stream) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!d_ods_rows || !d_row_block || !d_err) return e.fail(CDA_ERR_INVALID, "null buffer");
+        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        return e.enqueue_split_rows(static_cast<const uint8_t*>(d_ods_rows), k, n_rows, row0,
+                                    static_cast<uint8_t*>(d_row_block), d_err, s);
+    });
+}
+
+int cda_split_cols(cda_ctx* ctx, void* d_col_block, uint32_t k, uint32_t n_cols, uint32_t col0,
+                   void* d_col_root_slots, void* d_row_subtree_slots, uint32_t* d_err, void* stream) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!d_col_block || !d_col_root_slots || !d_row_subtree_slots || !d_err)
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        return e.enqueue_split_cols(static_cast<uint8_t*>(d_col_block), k, n_cols, col0,
+                                    static_cast<uint8_t*>(d_col_root_slots), static_cast<uint8_t*>(d_row_subtree_slots),
+                                    d_err, s);
+    });
+}
+
+int cda_split_combine(cda_ctx* ctx, const void* d_row_subtree_slots, uint32_t parts, uint32_t k,
+                      const void* d_col_root_slots, void* d_row_roots, void* d_col_roots, void* d_data_root,
+                      void* stream) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!d_row_subtree_slots || !d_col_root_slots || !d_row_roots || !d_col_roots || !d_data_root)
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        return e.enqueue_split_combine(static_cast<const uint8_t*>(d_row_subtree_slots), parts, k,
+                                       static_cast<const uint8_t*>(d_col_root_slots),
+                                       static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
+                                       static_cast<uint8_t*>(d_data_root), s);
+    });
+}
+
 int cda_set_profiling(cda_ctx* ctx, int enable) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
         e.set_profiling(enable != 0);

@@ -1,23 +1,34 @@
 // cda_kernels.h -- launch interface of the HIP kernels (engine <-> kernels).
+//
+// All kernels address shares through small descriptors of byte offsets so the
+// same code serves whole squares (configs 1-4), the row/column blocks of a
+// square split across GPUs (config 5) and rsmt2d Codec.Encode batches.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace cda {
 
-// Phase of the 2-D extension (rsmt2d erasureExtendSquare schedule):
-//   kPhaseQ0: codewords 0..k-1 = ODS rows (Q0->Q1, also copies Q0 into the EDS),
-//             codewords k..2k-1 = ODS columns (Q0->Q2);
-//   kPhaseQ3: codewords 0..k-1 = EDS rows k..2k-1 (Q2->Q3).
-enum RsPhase : int { kPhaseQ0 = 0, kPhaseQ3 = 1 };
+constexpr uint32_t kNoCopy = 0xFFFFFFFFu;
 
-// GF(2^8) Leopard encode of whole squares (k <= 128).
-hipError_t launch_rs8(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t n_squares, int phase,
-                      hipStream_t stream);
-// GF(2^8) encode of an arbitrary list of codewords: n_code codewords of k
-// shards x len bytes, contiguous (rsmt2d Codec.Encode compatibility).
-hipError_t launch_rs8_flat(const uint8_t* data, uint8_t* parity, uint32_t k, uint32_t len, uint32_t n_code,
-                           hipStream_t stream);
+// One group of codewords: codeword c, shard i lives at
+//   base + off + c*cw + i*sh   (bytes; offsets are per square and < 4 GiB).
+// `cpy_*` optionally stores the data shards unchanged (ODS -> EDS Q0 copy).
+struct RsSeg {
+    uint32_t n_cw;
+    uint32_t src_off, src_cw, src_sh;
+    uint32_t dst_off, dst_cw, dst_sh;
+    uint32_t cpy_off = kNoCopy, cpy_cw = 0, cpy_sh = 0;
+};
+// Up to two segments per launch (e.g. rows and columns of Q0 in one grid);
+// blockIdx.y selects the square: src + y*src_sq, dst + y*dst_sq.
+struct RsJob {
+    const uint8_t* src;
+    uint8_t* dst;           // parity and copy destination
+    uint64_t src_sq, dst_sq;
+    RsSeg seg[2];
+    uint32_t n_seg;
+};
 
 // GF(2^16) tables uploaded once per context.
 struct Gf16Dev {
@@ -30,32 +41,69 @@ struct Gf16Dev {
     const uint32_t* chunk = nullptr;
     uint32_t chunk_k = 0;
 };
-hipError_t launch_rs16(const Gf16Dev& t, const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t n_squares,
-                       int phase, hipStream_t stream);
+
+// Leopard encode of every codeword of `job` for n_squares squares; k data
+// shards of 512 B per codeword (GF(2^8) for k <= 128, GF(2^16) above).
+hipError_t launch_rs(const RsJob& job, uint32_t k, uint32_t n_squares, const Gf16Dev& gf16, hipStream_t stream);
+// rsmt2d Codec.Encode of n_code contiguous codewords of k shards x len bytes.
+hipError_t launch_rs8_flat(const uint8_t* data, uint8_t* parity, uint32_t k, uint32_t len, uint32_t n_code,
+                           hipStream_t stream);
 hipError_t launch_rs16_flat(const Gf16Dev& t, const uint8_t* data, uint8_t* parity, uint32_t k, uint32_t len,
                             uint32_t n_code, hipStream_t stream);
 
-// Q0 namespace order check: err[s] = min over violations of
-// (axis << 24 | axis_index << 12 | push_position), 0xFFFFFFFF when ordered.
-hipError_t launch_order_check(const uint8_t* eds, uint32_t k, uint32_t n_squares, uint32_t* err,
-                              hipStream_t stream);
+// Square phases (rsmt2d erasureExtendSquare): Q0->Q1 rows + Q0->Q2 columns
+// (with the Q0 copy), then Q2->Q3 rows.
+RsJob square_job_q0(const uint8_t* ods, uint8_t* eds, uint32_t k);
+RsJob square_job_q3(uint8_t* eds, uint32_t k);
+
+// A grid of EDS cells seen by the hash kernels: cell (r, c) of square y at
+//   base + y*sq + (r*row_stride + c)*512, global coordinates (row0 + r, col0 + c),
+// quadrant Q0 when row0+r < k and col0+c < k.
+struct CellGrid {
+    const uint8_t* base;
+    uint64_t sq;            // bytes per square
+    uint32_t rows, cols, row_stride;
+    uint32_t row0, col0, k;
+};
+
+// NMT leaf hashing: one 96-B leaf slot per grid cell, slots[y][r][c].  Also
+// checks nmt push order inside Q0: along rows if check_rows (both cells in the
+// grid) and along columns if check_cols.  err[y] = min over violations of
+// (axis << 24 | axis_index << 12 | push_position) in global coordinates.
+hipError_t launch_leaves(const CellGrid& g, uint32_t n_squares, uint8_t* slots, uint32_t* err, bool check_rows,
+                         bool check_cols, hipStream_t stream);
+// Push-order check of Q0 rows only, for a block of ODS rows held in
+// row-major order (config 5: each rank checks the rows it owns).
+hipError_t launch_row_order(const CellGrid& g, uint32_t n_squares, uint32_t* err, hipStream_t stream);
+
+// A forest of NMT trees over 96-B slots: node i of tree t of square y at
+//   in + y*in_sq + (t*tree_stride + i*node_stride)*96.
+// One level halves every tree: parent p of tree t goes to
+//   out + y*out_sq + (t*n_in/2 + p)*96;
+// when n_in == 2 the tree roots are written instead as packed 90-B nodes to
+// roots + y*roots_sq + (root0 + t)*90 (if roots) and as 96-B slots to
+// root_slots + y*rslot_sq + (root0 + t)*96 (if root_slots).
+struct Forest {
+    const uint8_t* in;
+    uint64_t in_sq;
+    uint32_t n_trees, tree_stride, node_stride;
+    uint8_t* out;
+    uint64_t out_sq;
+    uint8_t* roots;
+    uint64_t roots_sq;
+    uint8_t* root_slots;
+    uint64_t rslot_sq;
+    uint32_t root0;
+};
+// One level of up to two forests with the same n_in (blockIdx.z selects).
+hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n_squares, hipStream_t stream);
+// RFC-6962 data root over n_items 96-B root slots per square (power of two).
+hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares, uint8_t* data_roots,
+                            hipStream_t stream);
+// Pack n_slots 96-B root slots (rows then columns) into 90-B roots.
+hipError_t launch_slots_to_roots(const uint8_t* slots, uint32_t n_slots, uint8_t* rows, uint8_t* cols, uint32_t w,
+                                 hipStream_t stream);
 // err word -> CDA_OK (0) / CDA_ERR_PUSH_ORDER (-3) per square.
 hipError_t launch_status(const uint32_t* err, uint32_t n_squares, int32_t* status, hipStream_t stream);
-// NMT leaf hashing: one 96-B leaf slot per EDS cell, [n][W][W]; also runs the
-// Q0 push-order check (same err encoding as launch_order_check).
-hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n_squares, uint8_t* leaf_slots, uint32_t* err,
-                         hipStream_t stream);
-// One NMT level for all 2W trees of every square.  `in_leaf` selects the
-// level-0 addressing (row tree t = leaf row t, column tree t = leaf column t);
-// otherwise `in` is [n][2W][n_in] slots (rows then columns).  Output is
-// [n][2W][n_in/2] slots; when n_in == 2 the roots are written as packed
-// 90-byte nodes to row_roots/col_roots ([n][W][90]) and as 96-B slots to
-// root_slots ([n][2W][96], rows then columns) instead.
-hipError_t launch_level(const uint8_t* in, bool in_leaf, uint32_t W, uint32_t n_in, uint32_t n_squares,
-                        uint8_t* out, uint8_t* row_roots, uint8_t* col_roots, uint8_t* root_slots,
-                        hipStream_t stream);
-// RFC-6962 data root of rows || cols per square (reads root_slots).
-hipError_t launch_data_root(const uint8_t* root_slots, uint32_t W, uint32_t n_squares, uint8_t* data_roots,
-                            hipStream_t stream);
 
 }  // namespace cda

@@ -48,6 +48,14 @@ class Engine {
                     uint32_t* d_err, int32_t* d_status, hipStream_t s);
     int enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n, hipStream_t s);
 
+    // Config 5: one square split across ranks (cda_split_* in include/cda.h).
+    int enqueue_split_rows(const uint8_t* d_rows, uint32_t k, uint32_t n_rows, uint32_t row0, uint8_t* d_block,
+                           uint32_t* d_err, hipStream_t s);
+    int enqueue_split_cols(uint8_t* d_block, uint32_t k, uint32_t n_cols, uint32_t col0, uint8_t* d_col_slots,
+                           uint8_t* d_row_sub, uint32_t* d_err, hipStream_t s);
+    int enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint32_t k, const uint8_t* d_col_slots,
+                              uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_root, hipStream_t s);
+
     // Host-buffer helpers (copy in, run, copy out, synchronise).
     int host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
                         uint8_t* roots, int32_t* status);
@@ -66,6 +74,8 @@ class Engine {
 
   private:
     int check(hipError_t e, const char* what);
+    int run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
+                    uint64_t buf_sq, const uint64_t* out_off, hipStream_t s);
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,
                          bool src_is_eds);
 

@@ -167,21 +167,35 @@ int Engine::collect_stage_times(double* ms, uint32_t* counts, int n) {
 int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s) {
     if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
     int rc;
-    if (k <= 128) {
-        mark_begin(kStageRsQ0, s);
-        if ((rc = check(launch_rs8(d_ods, d_eds, k, n, kPhaseQ0, s), "rs8 Q0"))) return rc;
-        mark_end(s);
-        mark_begin(kStageRsQ3, s);
-        if ((rc = check(launch_rs8(d_ods, d_eds, k, n, kPhaseQ3, s), "rs8 Q3"))) return rc;
-        mark_end(s);
-    } else {
-        const Gf16Dev t = gf16(k);
-        mark_begin(kStageRsQ0, s);
-        if ((rc = check(launch_rs16(t, d_ods, d_eds, k, n, kPhaseQ0, s), "rs16 Q0"))) return rc;
-        mark_end(s);
-        mark_begin(kStageRsQ3, s);
-        if ((rc = check(launch_rs16(t, d_ods, d_eds, k, n, kPhaseQ3, s), "rs16 Q3"))) return rc;
-        mark_end(s);
+    const Gf16Dev t = gf16(k);
+    mark_begin(kStageRsQ0, s);
+    if ((rc = check(launch_rs(square_job_q0(d_ods, d_eds, k), k, n, t, s), "rs Q0"))) return rc;
+    mark_end(s);
+    mark_begin(kStageRsQ3, s);
+    if ((rc = check(launch_rs(square_job_q3(d_eds, k), k, n, t, s), "rs Q3"))) return rc;
+    mark_end(s);
+    return CDA_OK;
+}
+
+// Run every level of `f` (n_forest forests of n_in leaves each) ping-ponging
+// between two scratch buffers; the first level reads f[i].in.
+int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
+                        uint64_t buf_sq, const uint64_t* out_off, hipStream_t s) {
+    uint8_t* out = bufA;
+    int rc;
+    for (uint32_t m = n_in; m >= 2; m /= 2) {
+        for (uint32_t i = 0; i < n_forest; i++) {
+            f[i].out = out + out_off[i];
+            f[i].out_sq = buf_sq;
+        }
+        if ((rc = check(launch_level(f, n_forest, m, n, s), "nmt level"))) return rc;
+        for (uint32_t i = 0; i < n_forest; i++) {   // next level reads this one
+            f[i].in = out + out_off[i];
+            f[i].in_sq = buf_sq;
+            f[i].tree_stride = m / 2;
+            f[i].node_stride = 1;
+        }
+        out = out == bufA ? bufB : bufA;
     }
     return CDA_OK;
 }
@@ -190,34 +204,104 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
                         uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s) {
     if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
     const uint32_t W = 2 * k;
-    const size_t slots = (size_t)n * W * W * kSlot;
+    const uint64_t slots_sq = (uint64_t)W * W * kSlot;
     int rc;
-    if ((rc = check(leaf_.ensure(slots), "hipMalloc leaf slots"))) return rc;
-    if ((rc = check(lvl_.ensure(slots), "hipMalloc level slots"))) return rc;
+    if ((rc = check(leaf_.ensure(slots_sq * n), "hipMalloc leaf slots"))) return rc;
+    if ((rc = check(lvl_.ensure(slots_sq * n), "hipMalloc level slots"))) return rc;
     if ((rc = check(root_slots_.ensure((size_t)n * 2 * W * kSlot), "hipMalloc root slots"))) return rc;
     if ((rc = check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync"))) return rc;
     mark_begin(kStageLeaves, s);
-    if ((rc = check(launch_leaves(d_eds, k, n, leaf_.as<uint8_t>(), d_err, s), "leaf hashing"))) return rc;
+    const CellGrid g{d_eds, (uint64_t)W * W * kShare, W, W, W, 0, 0, k};
+    if ((rc = check(launch_leaves(g, n, leaf_.as<uint8_t>(), d_err, true, true, s), "leaf hashing"))) return rc;
     mark_end(s);
     mark_begin(kStageLevels, s);
-    uint8_t* in = leaf_.as<uint8_t>();
-    uint8_t* out = lvl_.as<uint8_t>();
-    bool in_leaf = true;
-    for (uint32_t n_in = W; n_in >= 2; n_in /= 2) {
-        if ((rc = check(launch_level(in, in_leaf, W, n_in, n, out, d_rows, d_cols, root_slots_.as<uint8_t>(), s),
-                        "nmt level")))
-            return rc;
-        uint8_t* t = in;
-        in = out;
-        out = t;
-        in_leaf = false;
-    }
+    // row trees: leaves (t, i); column trees: leaves (i, t) of the same leaf grid
+    Forest f[2]{};
+    f[0] = Forest{leaf_.as<uint8_t>(), slots_sq, W, W, 1, nullptr, 0, d_rows, (uint64_t)W * kNode,
+                  root_slots_.as<uint8_t>(), (uint64_t)2 * W * kSlot, 0};
+    f[1] = Forest{leaf_.as<uint8_t>(), slots_sq, W, 1, W, nullptr, 0, d_cols, (uint64_t)W * kNode,
+                  root_slots_.as<uint8_t>(), (uint64_t)2 * W * kSlot, W};
+    const uint64_t off[2] = {0, slots_sq / 2};
+    if ((rc = run_forests(f, 2, W, n, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), slots_sq, off, s))) return rc;
     mark_end(s);
     mark_begin(kStageDataRoot, s);
-    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), W, n, d_roots, s), "data root"))) return rc;
+    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), 2 * W, n, d_roots, s), "data root"))) return rc;
     mark_end(s);
     if (d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
     return CDA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Config 5: one square split across G ranks (see include/cda.h cda_split_*).
+// ---------------------------------------------------------------------------
+int Engine::enqueue_split_rows(const uint8_t* d_rows, uint32_t k, uint32_t n_rows, uint32_t row0, uint8_t* d_block,
+                               uint32_t* d_err, hipStream_t s) {
+    if (!pow2(k) || k > 1024 || n_rows == 0 || row0 + n_rows > k)
+        return fail(CDA_ERR_INVALID, "bad row block");
+    const uint32_t W = 2 * k, SH = kShare;
+    int rc;
+    const CellGrid g{d_rows, 0, n_rows, k, k, row0, 0, k};
+    if ((rc = check(launch_row_order(g, 1, d_err, s), "row order"))) return rc;
+    RsJob j{};
+    j.src = d_rows;
+    j.dst = d_block;
+    j.n_seg = 1;
+    j.seg[0] = RsSeg{n_rows, 0, k * SH, SH, k * SH, W * SH, SH, 0, W * SH, SH};
+    return check(launch_rs(j, k, 1, gf16(k), s), "rs rows");
+}
+
+int Engine::enqueue_split_cols(uint8_t* d_block, uint32_t k, uint32_t n_cols, uint32_t col0, uint8_t* d_col_slots,
+                               uint8_t* d_row_sub, uint32_t* d_err, hipStream_t s) {
+    const uint32_t W = 2 * k, SH = kShare;
+    if (!pow2(k) || k > 1024 || !pow2(n_cols) || n_cols < 2 || col0 + n_cols > W)
+        return fail(CDA_ERR_INVALID, "bad column block");
+    int rc;
+    RsJob j{};
+    j.src = d_block;
+    j.dst = d_block;
+    j.n_seg = 1;
+    j.seg[0] = RsSeg{n_cols, 0, SH, n_cols * SH, k * n_cols * SH, SH, n_cols * SH};
+    if ((rc = check(launch_rs(j, k, 1, gf16(k), s), "rs cols"))) return rc;
+    const uint64_t slots = (uint64_t)W * n_cols * kSlot;
+    if ((rc = check(leaf_.ensure(slots), "hipMalloc leaf slots"))) return rc;
+    if ((rc = check(lvl_.ensure(slots), "hipMalloc level slots"))) return rc;
+    const CellGrid g{d_block, 0, W, n_cols, n_cols, 0, col0, k};
+    if ((rc = check(launch_leaves(g, 1, leaf_.as<uint8_t>(), d_err, true, true, s), "leaf hashing"))) return rc;
+    // row subtrees: W trees of n_cols leaves -> one 96-B slot per row
+    // (ping-pong between the two halves of the level buffer; leaves untouched)
+    Forest fr{leaf_.as<uint8_t>(), 0, W, n_cols, 1, nullptr, 0, nullptr, 0, d_row_sub, 0, 0};
+    const uint64_t off0[1] = {0};
+    if ((rc = run_forests(&fr, 1, n_cols, 1, lvl_.as<uint8_t>(), lvl_.as<uint8_t>() + slots / 2, 0, off0, s)))
+        return rc;
+    // column trees: n_cols trees of W leaves; after their first level the leaf
+    // buffer is free and becomes the second ping-pong buffer
+    Forest fc{leaf_.as<uint8_t>(), 0, n_cols, 1, n_cols, nullptr, 0, nullptr, 0, d_col_slots, 0, 0};
+    return run_forests(&fc, 1, W, 1, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), 0, off0, s);
+}
+
+int Engine::enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint32_t k, const uint8_t* d_col_slots,
+                                  uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_root, hipStream_t s) {
+    const uint32_t W = 2 * k;
+    if (!pow2(k) || !pow2(parts) || parts > W) return fail(CDA_ERR_INVALID, "bad split");
+    int rc;
+    if ((rc = check(root_slots_.ensure((size_t)2 * W * kSlot), "hipMalloc root slots"))) return rc;
+    if ((rc = check(lvl_.ensure((size_t)W * parts * kSlot), "hipMalloc level slots"))) return rc;
+    if ((rc = check(leaf_.ensure((size_t)W * parts * kSlot), "hipMalloc leaf slots"))) return rc;
+    uint8_t* rs = root_slots_.as<uint8_t>();
+    if (parts == 1) {
+        if ((rc = check(hipMemcpyAsync(rs, d_row_sub, (size_t)W * kSlot, hipMemcpyDeviceToDevice, s), "copy")))
+            return rc;
+    } else {
+        // row tree r: nodes (g, r) of [parts][W] -> top log2(parts) levels
+        Forest fr{d_row_sub, 0, W, 1, W, nullptr, 0, nullptr, 0, rs, 0, 0};
+        const uint64_t off0[1] = {0};
+        if ((rc = run_forests(&fr, 1, parts, 1, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), 0, off0, s))) return rc;
+    }
+    if ((rc = check(hipMemcpyAsync(rs + (size_t)W * kSlot, d_col_slots, (size_t)W * kSlot, hipMemcpyDeviceToDevice, s),
+                    "copy")))
+        return rc;
+    if ((rc = check(launch_slots_to_roots(rs, 2 * W, d_rows, d_cols, W, s), "pack roots"))) return rc;
+    return check(launch_data_root(rs, 2 * W, 1, d_root, s), "data root");
 }
 
 int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
@@ -240,8 +324,7 @@ int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uin
         return check(hipMemcpyAsync(d_parity, d_data, (size_t)len * n, hipMemcpyDeviceToDevice, s), "copy");
     if (k <= 128) return check(launch_rs8_flat(d_data, d_parity, k, len, n, s), "rs8 flat");
     if (k > 1024) return fail(CDA_ERR_UNSUPPORTED, "more than 2048 shards");
-    Gf16Dev t{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
-    return check(launch_rs16_flat(t, d_data, d_parity, k, len, n, s), "rs16 flat");
+    return check(launch_rs16_flat(gf16(k), d_data, d_parity, k, len, n, s), "rs16 flat");
 }
 
 // Build the reference's error text for the first violating square.
@@ -363,7 +446,7 @@ int Engine::host_data_root(const uint8_t* rows, const uint8_t* cols, uint32_t w,
     hipStream_t s = stream_;
     if ((rc = check(hipMemcpyAsync(root_slots_.ptr, slots.data(), slots.size(), hipMemcpyHostToDevice, s), "H2D")))
         return rc;
-    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), w, 1, h_roots_.as<uint8_t>(), s), "data root")))
+    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), 2 * w, 1, h_roots_.as<uint8_t>(), s), "data root")))
         return rc;
     if ((rc = check(hipMemcpyAsync(root, h_roots_.ptr, 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     return check(hipStreamSynchronize(s), "hipStreamSynchronize");

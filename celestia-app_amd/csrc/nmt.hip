@@ -70,41 +70,35 @@ __device__ __forceinline__ bool ns_less(const uint32_t (&a)[8], const uint32_t (
     return false;
 }
 
-__global__ __launch_bounds__(256) void order_kernel(const uint8_t* __restrict__ eds, uint32_t k,
-                                                   uint32_t* __restrict__ err) {
-    const uint32_t W = 2 * k;
+// Row-only push-order check over a grid of Q0 cells (config 5: the rank that
+// owns a block of ODS rows checks them whole).
+__global__ __launch_bounds__(256) void row_order_kernel(const CellGrid g, uint32_t* __restrict__ err) {
     const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
-    if (cell >= k * k) return;
-    const size_t sq = blockIdx.y;
-    const uint32_t r = cell / k, c = cell % k;
-    const uint8_t* E = eds + sq * (size_t)W * W * SH;
+    if (cell >= g.rows * g.cols) return;
+    const uint32_t r = cell / g.cols, c = cell % g.cols;
+    const uint32_t gr = g.row0 + r, gc = g.col0 + c;
+    if (gr >= g.k || gc + 1 >= g.k || c + 1 >= g.cols) return;
+    const uint8_t* E = g.base + blockIdx.y * g.sq;
     uint32_t me[8], nb[8];
-    load_ns_be(E + ((size_t)r * W + c) * SH, me);
-    uint32_t key = 0xFFFFFFFFu;
-    if (c + 1 < k) {
-        load_ns_be(E + ((size_t)r * W + c + 1) * SH, nb);
-        if (ns_less(nb, me)) key = min(key, (0u << 24) | (r << 12) | (c + 1));
-    }
-    if (r + 1 < k) {
-        load_ns_be(E + ((size_t)(r + 1) * W + c) * SH, nb);
-        if (ns_less(nb, me)) key = min(key, (1u << 24) | (c << 12) | (r + 1));
-    }
-    if (key != 0xFFFFFFFFu) atomicMin(err + sq, key);
+    load_ns_be(E + ((size_t)r * g.row_stride + c) * SH, me);
+    load_ns_be(E + ((size_t)r * g.row_stride + c + 1) * SH, nb);
+    if (ns_less(nb, me)) atomicMin(err + blockIdx.y, (0u << 24) | (gr << 12) | (gc + 1));
 }
 
 // ---------------------------------------------------------------------------
 // Leaf hashing: one thread per EDS cell, 9 SHA-256 blocks of
 // 0x00 || ns || share, share streamed in 64-B chunks (prefetch one ahead).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void leaf_kernel(const uint8_t* __restrict__ eds, uint32_t k,
-                                                  uint8_t* __restrict__ slots, uint32_t* __restrict__ err) {
-    const uint32_t W = 2 * k;
+__global__ __launch_bounds__(256) void leaf_kernel(const CellGrid g, uint8_t* __restrict__ slots,
+                                                  uint32_t* __restrict__ err, int check_rows, int check_cols) {
     const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
-    if (cell >= W * W) return;
+    if (cell >= g.rows * g.cols) return;
     const size_t sq = blockIdx.y;
-    const uint32_t r = cell / W, c = cell % W;
-    const bool parity = !(r < k && c < k);
-    const uint4* src = reinterpret_cast<const uint4*>(eds + (sq * (size_t)W * W + cell) * SH);
+    const uint32_t r = cell / g.cols, c = cell % g.cols;
+    const uint32_t gr = g.row0 + r, gc = g.col0 + c, k = g.k;
+    const bool parity = !(gr < k && gc < k);
+    const uint8_t* E = g.base + sq * g.sq;
+    const uint4* src = reinterpret_cast<const uint4*>(E + ((size_t)r * g.row_stride + c) * SH);
 
     ShaState st;
     sha_init(st);
@@ -145,7 +139,7 @@ __global__ __launch_bounds__(256) void leaf_kernel(const uint8_t* __restrict__ e
 
     uint32_t out[kSlotWords];
     leaf_node_words(nsw, st.h, out);
-    store_slot(slots + (sq * (size_t)W * W + cell) * kSlot, out);
+    store_slot(slots + (sq * (size_t)g.rows * g.cols + cell) * kSlot, out);
 
     // nmt push-order check of Q0 (fused: this cell's namespace is in nsw)
     if (!parity) {
@@ -153,50 +147,45 @@ __global__ __launch_bounds__(256) void leaf_kernel(const uint8_t* __restrict__ e
 #pragma unroll
         for (int i = 0; i < 7; i++) me[i] = nsw[i];
         me[7] = nsw[7] & 0xFF000000u;
-        const uint8_t* E = eds + sq * (size_t)W * W * SH;
         uint32_t key = 0xFFFFFFFFu;
-        if (c + 1 < k) {
-            load_ns_be(E + ((size_t)r * W + c + 1) * SH, nb);
-            if (ns_less(nb, me)) key = min(key, (0u << 24) | (r << 12) | (c + 1));
+        if (check_rows && gc + 1 < k && c + 1 < g.cols) {
+            load_ns_be(E + ((size_t)r * g.row_stride + c + 1) * SH, nb);
+            if (ns_less(nb, me)) key = min(key, (0u << 24) | (gr << 12) | (gc + 1));
         }
-        if (r + 1 < k) {
-            load_ns_be(E + ((size_t)(r + 1) * W + c) * SH, nb);
-            if (ns_less(nb, me)) key = min(key, (1u << 24) | (c << 12) | (r + 1));
+        if (check_cols && gr + 1 < k && r + 1 < g.rows) {
+            load_ns_be(E + ((size_t)(r + 1) * g.row_stride + c) * SH, nb);
+            if (ns_less(nb, me)) key = min(key, (1u << 24) | (gc << 12) | (gr + 1));
         }
         if (key != 0xFFFFFFFFu) atomicMin(err + sq, key);
     }
 }
 
 // ---------------------------------------------------------------------------
-// One NMT level.  blockIdx.z = axis (0 rows, 1 columns).
+// One NMT level of up to two forests (blockIdx.z).  Thread -> (tree, parent):
+// parents of one tree are adjacent threads when nodes are adjacent slots
+// (node_stride == 1), otherwise adjacent threads take the same parent of
+// adjacent trees (tree_stride == 1, e.g. column trees over a row-major grid),
+// so slot loads stay coalesced either way.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void level_kernel(const uint8_t* __restrict__ in, int in_leaf, uint32_t W,
-                                                   uint32_t n_in, uint8_t* __restrict__ out,
-                                                   uint8_t* __restrict__ row_roots, uint8_t* __restrict__ col_roots,
-                                                   uint8_t* __restrict__ root_slots) {
+struct Forest2 {
+    Forest f[2];
+};
+
+__global__ __launch_bounds__(256) void level_kernel(const Forest2 fs, uint32_t n_in) {
+    const Forest& F = fs.f[blockIdx.z];
     const uint32_t n_out = n_in / 2;
     const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= W * n_out) return;
-    const uint32_t axis = blockIdx.z;
+    if (idx >= F.n_trees * n_out) return;
     const size_t sq = blockIdx.y;
     uint32_t t, p;
-    const uint8_t *l, *rr;
-    if (in_leaf) {
-        const uint8_t* base = in + sq * (size_t)W * W * kSlot;
-        if (axis == 0) {  // row tree t: leaves (t, i)
-            t = idx / n_out; p = idx % n_out;
-            l = base + ((size_t)t * W + 2 * p) * kSlot;
-            rr = l + kSlot;
-        } else {          // column tree t: leaves (i, t); consecutive threads = consecutive trees
-            p = idx / W; t = idx % W;
-            l = base + ((size_t)(2 * p) * W + t) * kSlot;
-            rr = l + (size_t)W * kSlot;
-        }
-    } else {
+    if (F.node_stride == 1) {
         t = idx / n_out; p = idx % n_out;
-        l = in + ((sq * 2 + axis) * W + t) * (size_t)n_in * kSlot + (size_t)(2 * p) * kSlot;
-        rr = l + kSlot;
+    } else {
+        p = idx / F.n_trees; t = idx % F.n_trees;
     }
+    const uint8_t* base = F.in + sq * F.in_sq;
+    const uint8_t* l = base + ((size_t)t * F.tree_stride + (size_t)(2 * p) * F.node_stride) * kSlot;
+    const uint8_t* rr = l + (size_t)F.node_stride * kSlot;
     uint32_t L[kSlotWords], R[kSlotWords], w[16];
     load_slot_be(l, L);
     load_slot_be(rr, R);
@@ -211,13 +200,14 @@ __global__ __launch_bounds__(256) void level_kernel(const uint8_t* __restrict__ 
     uint32_t o[kSlotWords];
     inner_node_words(L, R, st.h, o);
     if (n_out == 1) {
-        uint8_t* dst = (axis == 0 ? row_roots : col_roots) + (sq * W + t) * (size_t)kNode;
-        uint16_t* d16 = reinterpret_cast<uint16_t*>(dst);   // 90-byte packed roots are 2-B aligned
+        if (F.roots) {
+            uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)(F.root0 + t) * kNode);
 #pragma unroll
-        for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
-        store_slot(root_slots + ((sq * 2 + axis) * W + t) * (size_t)kSlot, o);
+            for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
+        }
+        if (F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
     } else {
-        store_slot(out + ((sq * 2 + axis) * W + t) * (size_t)n_out * kSlot + (size_t)p * kSlot, o);
+        store_slot(F.out + sq * F.out_sq + ((size_t)t * n_out + p) * kSlot, o);
     }
 }
 
@@ -225,11 +215,10 @@ __global__ __launch_bounds__(256) void level_kernel(const uint8_t* __restrict__ 
 // Data root: RFC-6962 over the 2W root slots (rows then columns); 2W is a
 // power of two so the tree is perfect.  One 256-thread block per square.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void data_root_kernel(const uint8_t* __restrict__ root_slots, uint32_t W,
+__global__ __launch_bounds__(256) void data_root_kernel(const uint8_t* __restrict__ root_slots, uint32_t n,
                                                        uint8_t* __restrict__ data_roots) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // ping [2W][8] | pong [W][8]
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // ping [n][8] | pong [n/2][8]
     const size_t sq = blockIdx.x;
-    const uint32_t n = 2 * W;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         uint32_t I[kSlotWords], w[16];
         load_slot_be(root_slots + (sq * n + i) * (size_t)kSlot, I);
@@ -278,44 +267,67 @@ __global__ void status_kernel(const uint32_t* __restrict__ err, uint32_t n, int3
     if (i < n) status[i] = err[i] == 0xFFFFFFFFu ? 0 : -3;   // CDA_OK / CDA_ERR_PUSH_ORDER
 }
 
+__global__ void slots_to_roots_kernel(const uint8_t* __restrict__ slots, uint32_t n, uint8_t* __restrict__ rows,
+                                      uint8_t* __restrict__ cols, uint32_t w) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * (kNode / 2)) return;
+    const uint32_t node = i / (kNode / 2), h = i % (kNode / 2);
+    const uint16_t v = reinterpret_cast<const uint16_t*>(slots + (size_t)node * kSlot)[h];
+    uint8_t* dst = node < w ? rows + (size_t)node * kNode : cols + (size_t)(node - w) * kNode;
+    reinterpret_cast<uint16_t*>(dst)[h] = v;
+}
+
 }  // namespace
+
+hipError_t launch_slots_to_roots(const uint8_t* slots, uint32_t n, uint8_t* rows, uint8_t* cols, uint32_t w,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(slots_to_roots_kernel, dim3((n * (kNode / 2) + 255) / 256), dim3(256), 0, s, slots, n, rows,
+                       cols, w);
+    return hipGetLastError();
+}
 
 hipError_t launch_status(const uint32_t* err, uint32_t n, int32_t* status, hipStream_t s) {
     hipLaunchKernelGGL(status_kernel, dim3((n + 255) / 256), dim3(256), 0, s, err, n, status);
     return hipGetLastError();
 }
 
-hipError_t launch_order_check(const uint8_t* eds, uint32_t k, uint32_t n, uint32_t* err, hipStream_t s) {
-    dim3 grid((k * k + 255) / 256, n);
-    hipLaunchKernelGGL(order_kernel, grid, dim3(256), 0, s, eds, k, err);
+hipError_t launch_row_order(const CellGrid& g, uint32_t n, uint32_t* err, hipStream_t s) {
+    dim3 grid((g.rows * g.cols + 255) / 256, n);
+    hipLaunchKernelGGL(row_order_kernel, grid, dim3(256), 0, s, g, err);
     return hipGetLastError();
 }
 
-hipError_t launch_leaves(const uint8_t* eds, uint32_t k, uint32_t n, uint8_t* slots, uint32_t* err, hipStream_t s) {
-    const uint32_t W = 2 * k;
-    dim3 grid((W * W + 255) / 256, n);
-    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), 0, s, eds, k, slots, err);
+hipError_t launch_leaves(const CellGrid& g, uint32_t n, uint8_t* slots, uint32_t* err, bool check_rows,
+                         bool check_cols, hipStream_t s) {
+    dim3 grid((g.rows * g.cols + 255) / 256, n);
+    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), 0, s, g, slots, err, check_rows ? 1 : 0, check_cols ? 1 : 0);
     return hipGetLastError();
 }
 
-hipError_t launch_level(const uint8_t* in, bool in_leaf, uint32_t W, uint32_t n_in, uint32_t n, uint8_t* out,
-                        uint8_t* row_roots, uint8_t* col_roots, uint8_t* root_slots, hipStream_t s) {
-    const uint32_t per_axis = W * (n_in / 2);
-    dim3 grid((per_axis + 255) / 256, n, 2);
-    hipLaunchKernelGGL(level_kernel, grid, dim3(256), 0, s, in, in_leaf ? 1 : 0, W, n_in, out, row_roots, col_roots,
-                       root_slots);
+hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, hipStream_t s) {
+    if (n_forest < 1 || n_forest > 2 || n_in < 2) return hipErrorInvalidValue;
+    Forest2 fs{};
+    uint32_t maxw = 0;
+    for (uint32_t i = 0; i < n_forest; i++) {
+        fs.f[i] = f[i];
+        maxw = maxw > f[i].n_trees * (n_in / 2) ? maxw : f[i].n_trees * (n_in / 2);
+    }
+    dim3 grid((maxw + 255) / 256, n, n_forest);
+    hipLaunchKernelGGL(level_kernel, grid, dim3(256), 0, s, fs, n_in);
     return hipGetLastError();
 }
 
-hipError_t launch_data_root(const uint8_t* root_slots, uint32_t W, uint32_t n, uint8_t* data_roots, hipStream_t s) {
-    const size_t lds = (size_t)3 * W * 32;   // ping-pong: 2W + W digests
+hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_t n, uint8_t* data_roots,
+                            hipStream_t s) {
+    if (n_items < 2 || (n_items & (n_items - 1))) return hipErrorInvalidValue;
+    const size_t lds = (size_t)3 * (n_items / 2) * 32;   // ping-pong: n + n/2 digests
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(data_root_kernel),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(data_root_kernel, dim3(n), dim3(256), lds, s, root_slots, W, data_roots);
+    hipLaunchKernelGGL(data_root_kernel, dim3(n), dim3(256), lds, s, root_slots, n_items, data_roots);
     return hipGetLastError();
 }
 

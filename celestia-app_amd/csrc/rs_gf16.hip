@@ -136,40 +136,23 @@ __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], c
 }
 
 template <int K>
-__global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const uint8_t* __restrict__ ods,
-                                                      uint8_t* __restrict__ eds, int phase) {
+__global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const RsJob job) {
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
-    constexpr uint32_t W = 2 * K;
     const Tab16 T{tab};
-    const uint32_t cw = blockIdx.x;
-    const size_t sq = blockIdx.y;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t off = 64 * (lane >> 3) + 4 * (lane & 7);    // lo dword; hi at +32
     // All addressing is a uniform base pointer + a 32-bit byte offset (one
     // VGPR per access, saddr form), so no 64-bit address pairs stay live.
-    const uint8_t* src_base;
-    uint32_t s0, ss;                    // source: shard i at src_base + s0 + i*ss
-    uint8_t* E = eds + sq * (size_t)W * W * SH;
-    uint32_t d0, ds;                    // parity / scratch: shard i at E + d0 + i*ds
-    uint32_t c0 = 0xFFFFFFFFu;          // Q0 copy: shard i at E + c0 + i*SH
-    if (phase == kPhaseQ0) {
-        src_base = ods + sq * (size_t)K * K * SH;
-        if (cw < K) {
-            s0 = cw * K * (uint32_t)SH; ss = SH;
-            d0 = (cw * W + K) * (uint32_t)SH; ds = SH;
-            c0 = cw * W * (uint32_t)SH;
-        } else {
-            const uint32_t j = cw - K;
-            s0 = j * (uint32_t)SH; ss = K * (uint32_t)SH;
-            d0 = (K * W + j) * (uint32_t)SH; ds = W * (uint32_t)SH;
-        }
-    } else {
-        src_base = E;
-        s0 = (K + cw) * W * (uint32_t)SH; ss = SH;
-        d0 = ((K + cw) * W + K) * (uint32_t)SH; ds = SH;
-    }
+    const bool s1 = job.n_seg > 1 && blockIdx.x >= job.seg[0].n_cw;
+    const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
+    const uint32_t c = s1 ? blockIdx.x - job.seg[0].n_cw : blockIdx.x;
+    const uint8_t* src_base = job.src + blockIdx.y * job.src_sq;
+    uint8_t* E = job.dst + blockIdx.y * job.dst_sq;
+    const uint32_t s0 = g.src_off + c * g.src_cw, ss = g.src_sh;      // data shard i
+    const uint32_t d0 = g.dst_off + c * g.dst_cw, ds = g.dst_sh;      // parity / scratch shard i
+    const uint32_t c0 = g.cpy_off == kNoCopy ? kNoCopy : g.cpy_off + c * g.cpy_cw;
     // `lo_off` is re-laundered at every use site so the compiler recomputes
     // (one v_add) instead of keeping dozens of per-shard addresses live.
     auto lane_off = [&]() {
@@ -193,8 +176,8 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         uint32_t lo[S], hi[S];
         const uint32_t base = S * wave;
         sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (base + jj.value) * ss, lo[jj.value], hi[jj.value]); });
-        if (c0 != 0xFFFFFFFFu) {
-            sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * (uint32_t)SH, lo[jj.value], hi[jj.value]); });
+        if (c0 != kNoCopy) {
+            sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * g.cpy_sh, lo[jj.value], hi[jj.value]); });
         }
         ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + base; });
         sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
@@ -286,29 +269,20 @@ __device__ void encode_block_column(const Gf16Dev& t, uint16_t* sym, uint32_t k,
     }
 }
 
-__global__ __launch_bounds__(256) void rs16_lds_kernel(Gf16Dev t, const uint8_t* __restrict__ ods,
-                                                      uint8_t* __restrict__ eds, uint32_t k, int phase) {
+__global__ __launch_bounds__(256) void rs16_lds_kernel(Gf16Dev t, const RsJob job, uint32_t k) {
     extern __shared__ __attribute__((aligned(16))) uint16_t sym[];
-    const uint32_t W = 2 * k;
     const uint32_t cw = blockIdx.x >> 3;
     const uint32_t blk = blockIdx.x & 7;
-    const size_t sq = blockIdx.y;
-    const uint8_t* O = ods + sq * (size_t)k * k * SH;
-    uint8_t* E = eds + sq * (size_t)W * W * SH;
+    const bool s1 = job.n_seg > 1 && cw >= job.seg[0].n_cw;
+    const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
+    const uint32_t c = s1 ? cw - job.seg[0].n_cw : cw;
+    const uint8_t* src = job.src + blockIdx.y * job.src_sq;
+    uint8_t* dst = job.dst + blockIdx.y * job.dst_sq;
     const size_t off = (size_t)blk * 64;
-    if (phase == kPhaseQ0) {
-        if (cw < k) {
-            encode_block_column(t, sym, k, O + (size_t)cw * k * SH + off, SH, E + ((size_t)cw * W + k) * SH + off, SH,
-                                E + (size_t)cw * W * SH + off, SH);
-        } else {
-            const uint32_t j = cw - k;
-            encode_block_column(t, sym, k, O + (size_t)j * SH + off, (size_t)k * SH,
-                                E + ((size_t)k * W + j) * SH + off, (size_t)W * SH, nullptr, 0);
-        }
-    } else {
-        const uint8_t* src = E + (size_t)(k + cw) * W * SH + off;
-        encode_block_column(t, sym, k, src, SH, E + ((size_t)(k + cw) * W + k) * SH + off, SH, nullptr, 0);
-    }
+    encode_block_column(t, sym, k, src + (size_t)g.src_off + (size_t)c * g.src_cw + off, g.src_sh,
+                        dst + (size_t)g.dst_off + (size_t)c * g.dst_cw + off, g.dst_sh,
+                        g.cpy_off == kNoCopy ? nullptr : dst + (size_t)g.cpy_off + (size_t)c * g.cpy_cw + off,
+                        g.cpy_sh);
 }
 
 __global__ __launch_bounds__(256) void rs16_flat_kernel(Gf16Dev t, const uint8_t* __restrict__ data,
@@ -321,25 +295,27 @@ __global__ __launch_bounds__(256) void rs16_flat_kernel(Gf16Dev t, const uint8_t
 }
 
 template <int K>
-hipError_t launch_cw(const Gf16Dev& t, const uint8_t* ods, uint8_t* eds, uint32_t n, int phase, hipStream_t s) {
-    dim3 grid(phase == kPhaseQ0 ? 2 * K : K, n);
-    hipLaunchKernelGGL(rs16_cw_kernel<K>, grid, dim3(1024), 0, s, t.chunk, ods, eds, phase);
+hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s) {
+    const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
+    hipLaunchKernelGGL(rs16_cw_kernel<K>, dim3(ncw, n), dim3(1024), 0, s, t.chunk, j);
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_rs16(const Gf16Dev& t, const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t n, int phase,
-                       hipStream_t s) {
-    if (k < 2 || (k & (k - 1)) || k > 32768) return hipErrorInvalidValue;
+hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s);
+
+hipError_t launch_rs(const RsJob& j, uint32_t k, uint32_t n, const Gf16Dev& t, hipStream_t s) {
+    if (k == 0 || (k & (k - 1))) return hipErrorInvalidValue;
+    if (k <= 128) return launch_rs8_job(j, k, n, s);
     if (t.chunk && t.chunk_k == k) {
-        if (k == 256) return launch_cw<256>(t, ods, eds, n, phase, s);
-        if (k == 512) return launch_cw<512>(t, ods, eds, n, phase, s);
+        if (k == 256) return launch_cw<256>(t, j, n, s);
+        if (k == 512) return launch_cw<512>(t, j, n, s);
     }
     const size_t lds = (size_t)k * 64;
     if (lds > 64 * 1024) return hipErrorInvalidValue;
-    dim3 grid((phase == kPhaseQ0 ? 2 * k : k) * 8, n);
-    hipLaunchKernelGGL(rs16_lds_kernel, grid, dim3(256), lds, s, t, ods, eds, k, phase);
+    const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
+    hipLaunchKernelGGL(rs16_lds_kernel, dim3(ncw * 8, n), dim3(256), lds, s, t, j, k);
     return hipGetLastError();
 }
 

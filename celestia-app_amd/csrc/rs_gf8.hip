@@ -129,48 +129,40 @@ __device__ __forceinline__ void encode_regs(uint32_t (&v)[M]) {
 template <int K>
 constexpr int waves_per_simd() { return K >= 128 ? 2 : 4; }
 
+// Segment of codeword blockIdx.x (uniform) -> byte offsets.
+struct SegSel {
+    uint32_t s0, ss, d0, ds, c0;
+};
+__device__ __forceinline__ SegSel select_seg(const RsJob& j, uint32_t cw) {
+    const RsSeg& g = (j.n_seg > 1 && cw >= j.seg[0].n_cw) ? j.seg[1] : j.seg[0];
+    const uint32_t c = (j.n_seg > 1 && cw >= j.seg[0].n_cw) ? cw - j.seg[0].n_cw : cw;
+    SegSel r;
+    r.s0 = g.src_off + c * g.src_cw;
+    r.ss = g.src_sh;
+    r.d0 = g.dst_off + c * g.dst_cw;
+    r.ds = g.dst_sh;
+    r.c0 = g.cpy_off == kNoCopy ? kNoCopy : g.cpy_off + c * g.cpy_cw;
+    return r;
+}
+
 template <int K>
-__global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_square_kernel(const uint8_t* __restrict__ ods, uint8_t* __restrict__ eds,
-                                                        int phase) {
-    constexpr uint32_t W = 2 * K;
-    constexpr size_t SH = 512;
-    const uint32_t cw = blockIdx.x;
-    const size_t sq = blockIdx.y;
-    // Uniform base pointer + 32-bit byte offsets (saddr addressing).
+__global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_job_kernel(const RsJob job) {
+    constexpr uint32_t SH = 512;
+    const SegSel q = select_seg(job, blockIdx.x);
+    // Uniform base pointers + 32-bit byte offsets (saddr addressing).
+    const uint8_t* src = job.src + blockIdx.y * job.src_sq;
+    uint8_t* dst = job.dst + blockIdx.y * job.dst_sq;
     const uint32_t lane4 = threadIdx.x * 4;   // byte offset inside the 512-B shard
-    auto lane_off = [&]() { return lane4; };
-    const uint8_t* O = ods + sq * (size_t)K * K * SH;
-    uint8_t* E = eds + sq * (size_t)W * W * SH;
-    const uint8_t* src_base;
-    uint32_t s0, ss, d0, ds;
-    uint32_t c0 = 0xFFFFFFFFu;
-    if (phase == kPhaseQ0) {
-        src_base = O;
-        if (cw < K) {  // row cw: Q0 -> Q1 (and copy Q0 into the EDS)
-            s0 = cw * K * (uint32_t)SH; ss = SH;
-            d0 = (cw * W + K) * (uint32_t)SH; ds = SH;
-            c0 = cw * W * (uint32_t)SH;
-        } else {  // column j: Q0 -> Q2
-            const uint32_t j = cw - K;
-            s0 = j * (uint32_t)SH; ss = K * (uint32_t)SH;
-            d0 = (K * W + j) * (uint32_t)SH; ds = W * (uint32_t)SH;
-        }
-    } else {  // row K+cw: Q2 -> Q3
-        src_base = E;
-        s0 = (K + cw) * W * (uint32_t)SH; ss = SH;
-        d0 = ((K + cw) * W + K) * (uint32_t)SH; ds = SH;
-    }
     uint32_t v[K];
 #pragma unroll
-    for (int i = 0; i < K; i++)
-        v[i] = *reinterpret_cast<const uint32_t*>(src_base + (s0 + i * ss + lane_off()));
-    if (c0 != 0xFFFFFFFFu) {
+    for (int i = 0; i < K; i++) v[i] = *reinterpret_cast<const uint32_t*>(src + (q.s0 + i * q.ss + lane4));
+    if (q.c0 != kNoCopy) {
 #pragma unroll
-        for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(E + (c0 + i * (uint32_t)SH + lane_off())) = v[i];
+        for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(dst + (q.c0 + i * SH + lane4)) = v[i];
     }
     encode_regs<K>(v);
 #pragma unroll
-    for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(E + (d0 + i * ds + lane_off())) = v[i];
+    for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(dst + (q.d0 + i * q.ds + lane4)) = v[i];
 }
 
 // Flat codewords: codeword c = data[c*K*len ...], shards of len bytes.
@@ -192,9 +184,9 @@ __global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_flat_kernel(cons
 }
 
 template <int K>
-hipError_t launch_sq(const uint8_t* ods, uint8_t* eds, uint32_t n, int phase, hipStream_t s) {
-    dim3 grid(phase == kPhaseQ0 ? 2 * K : K, n);
-    hipLaunchKernelGGL(rs8_square_kernel<K>, grid, dim3(128), 0, s, ods, eds, phase);
+hipError_t launch_job(const RsJob& j, uint32_t n, hipStream_t s) {
+    const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
+    hipLaunchKernelGGL(rs8_job_kernel<K>, dim3(ncw, n), dim3(128), 0, s, j);
     return hipGetLastError();
 }
 template <int K>
@@ -206,18 +198,45 @@ hipError_t launch_fl(const uint8_t* d, uint8_t* p, uint32_t len, uint32_t n, hip
 
 }  // namespace
 
-hipError_t launch_rs8(const uint8_t* ods, uint8_t* eds, uint32_t k, uint32_t n, int phase, hipStream_t s) {
+hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s) {
     switch (k) {
-        case 1: return launch_sq<1>(ods, eds, n, phase, s);
-        case 2: return launch_sq<2>(ods, eds, n, phase, s);
-        case 4: return launch_sq<4>(ods, eds, n, phase, s);
-        case 8: return launch_sq<8>(ods, eds, n, phase, s);
-        case 16: return launch_sq<16>(ods, eds, n, phase, s);
-        case 32: return launch_sq<32>(ods, eds, n, phase, s);
-        case 64: return launch_sq<64>(ods, eds, n, phase, s);
-        case 128: return launch_sq<128>(ods, eds, n, phase, s);
+        case 1: return launch_job<1>(j, n, s);
+        case 2: return launch_job<2>(j, n, s);
+        case 4: return launch_job<4>(j, n, s);
+        case 8: return launch_job<8>(j, n, s);
+        case 16: return launch_job<16>(j, n, s);
+        case 32: return launch_job<32>(j, n, s);
+        case 64: return launch_job<64>(j, n, s);
+        case 128: return launch_job<128>(j, n, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+RsJob square_job_q0(const uint8_t* ods, uint8_t* eds, uint32_t k) {
+    const uint32_t W = 2 * k, SH = 512;
+    RsJob j{};
+    j.src = ods;
+    j.dst = eds;
+    j.src_sq = (uint64_t)k * k * SH;
+    j.dst_sq = (uint64_t)W * W * SH;
+    j.n_seg = 2;
+    // rows: ODS row c -> EDS row c (Q0 copy) and Q1
+    j.seg[0] = RsSeg{k, 0, k * SH, SH, k * SH, W * SH, SH, 0, W * SH, SH};
+    // columns: ODS column c -> Q2 column c
+    j.seg[1] = RsSeg{k, 0, SH, k * SH, k * W * SH, SH, W * SH};
+    return j;
+}
+
+RsJob square_job_q3(uint8_t* eds, uint32_t k) {
+    const uint32_t W = 2 * k, SH = 512;
+    RsJob j{};
+    j.src = eds;
+    j.dst = eds;
+    j.src_sq = j.dst_sq = (uint64_t)W * W * SH;
+    j.n_seg = 1;
+    // rows k..2k-1: Q2 -> Q3
+    j.seg[0] = RsSeg{k, k * W * SH, W * SH, SH, k * W * SH + k * SH, W * SH, SH};
+    return j;
 }
 
 hipError_t launch_rs8_flat(const uint8_t* d, uint8_t* p, uint32_t k, uint32_t len, uint32_t n, hipStream_t s) {

@@ -116,6 +116,31 @@ int cda_data_root(cda_ctx *ctx, const uint8_t *row_roots, const uint8_t *col_roo
  * axis index, and the leaf position whose push failed. */
 int cda_push_order_detail(cda_ctx *ctx, int32_t *axis, uint32_t *index, uint32_t *position);
 
+/* Config 5: ONE square split across G ranks (one GPU each), row blocks +
+ * column blocks.  k = ODS width, W = 2k, R = k/G rows and C = W/G columns per
+ * rank.  All pointers are device memory; calls only enqueue on `stream`.
+ * d_err is one uint32 per rank, initialised by the caller to 0xFFFFFFFF;
+ * push-order violations atomically lower it (encoding: axis<<24 | index<<12 |
+ * position, reduce with MIN across ranks).
+ *  1. cda_split_rows: ODS rows [row0, row0+R) (R x k shares, row-major) ->
+ *     row block (R x W shares: Q0 row | Q1 row), plus the Q0 row-order check.
+ *  2. caller: all-to-all of the row blocks' column slices (RCCL) so rank g
+ *     holds rows 0..k-1 of columns [g*C, g*C+C) as a W x C share block.
+ *  3. cda_split_cols: column-encode the block (Q0->Q2 / Q1->Q3), hash each
+ *     cell once, write the C column roots and, per EDS row, the NMT subtree
+ *     node over this rank's C columns (96-B slots, W of them).
+ *  4. caller: gather the subtree slots ([G][W][96]) and column root slots
+ *     ([W][96], rank order) on one rank.
+ *  5. cda_split_combine: top log2(G) levels of every row tree, pack roots,
+ *     data root. */
+int cda_split_rows(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
+                   void *d_row_block, uint32_t *d_err, void *stream);
+int cda_split_cols(cda_ctx *ctx, void *d_col_block, uint32_t k, uint32_t n_cols, uint32_t col0,
+                   void *d_col_root_slots, void *d_row_subtree_slots, uint32_t *d_err, void *stream);
+int cda_split_combine(cda_ctx *ctx, const void *d_row_subtree_slots, uint32_t parts, uint32_t k,
+                      const void *d_col_root_slots, void *d_row_roots, void *d_col_roots, void *d_data_root,
+                      void *stream);
+
 /* Stage timing (HIP events on the launch stream).  When enabled, every
  * enqueued stage is bracketed by events; cda_stage_times synchronises them and
  * returns, per stage, the summed milliseconds and launch counts since the

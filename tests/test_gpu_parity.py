@@ -137,3 +137,33 @@ def test_random_fixtures_on_gpu(ctx, k):
     assert hashlib.sha256(rows.tobytes()).hexdigest() == g["row_roots_sha256"]
     assert hashlib.sha256(cols.tobytes()).hexdigest() == g["col_roots_sha256"]
     assert dah.hash().hex() == g["data_root"]
+
+
+@pytest.mark.parametrize("k,parts", [(4, 2), (16, 4), (128, 8), (512, 8), (512, 2)])
+def test_split_square_loopback_on_gpu(ctx, k, parts):
+    """Config 5 kernels (row block -> column block -> subtree combine) on one
+    GPU with `parts` virtual ranks: bit-exact EDS columns, roots, data root."""
+    import torch
+    from celestia_da import dist as cdist
+    ods = coracle.random_square(k, 9)
+    dev = torch.device("cuda", 0)
+    ops = cdist.GpuSplitOps(ctx, dev)
+    cols_eds, (rows, cols, root, err) = cdist.extend_dah_split_loopback(torch.from_numpy(ods).to(dev), k, parts, ops)
+    torch.cuda.synchronize()
+    e_eds, e_rows, e_cols, e_root = coracle.cpu_baseline(ods, 16) if k >= 64 else coracle.extend_dah(ods)
+    assert int(err.item()) == 0xFFFFFFFF
+    assert root.cpu().numpy().tobytes() == e_root
+    assert np.array_equal(rows.cpu().numpy(), e_rows) and np.array_equal(cols.cpu().numpy(), e_cols)
+    assert np.array_equal(cols_eds.cpu().numpy().reshape(-1, 512), e_eds)
+
+
+def test_split_push_order_on_gpu(ctx):
+    import torch
+    from celestia_da import dist as cdist
+    k = 16
+    ods = coracle.random_square(k, 4).reshape(k, k, 512).copy()
+    ods[5, 9, :29], ods[5, 10, :29] = ods[5, 10, :29].copy(), ods[5, 9, :29].copy()
+    dev = torch.device("cuda", 0)
+    _, (_, _, _, err) = cdist.extend_dah_split_loopback(torch.from_numpy(ods.reshape(-1, 512)).to(dev), k, 4,
+                                                         cdist.GpuSplitOps(ctx, dev))
+    assert int(err.item()) == (0 << 24) | (5 << 12) | 10
