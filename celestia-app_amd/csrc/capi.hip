@@ -121,7 +121,7 @@ int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t 
         static thread_local cda::DevBuf err;   // per-thread err words (device)
         hipError_t he = err.ensure((size_t)n * 4);
         if (he != hipSuccess) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
-        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_extend_dah(static_cast<const uint8_t*>(d_ods), k, n, static_cast<uint8_t*>(d_eds),
                                     static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
                                     static_cast<uint8_t*>(d_data_roots), err.as<uint32_t>(), d_status, s);
@@ -165,7 +165,7 @@ int cda_split_rows(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_
                    void* d_row_block, uint32_t* d_err, void* stream) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
         if (!d_ods_rows || !d_row_block || !d_err) return e.fail(CDA_ERR_INVALID, "null buffer");
-        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_split_rows(static_cast<const uint8_t*>(d_ods_rows), k, n_rows, row0,
                                     static_cast<uint8_t*>(d_row_block), d_err, s);
     });
@@ -176,7 +176,7 @@ int cda_split_cols(cda_ctx* ctx, void* d_col_block, uint32_t k, uint32_t n_cols,
     return guarded(ctx, [&](cda::Engine& e) -> int {
         if (!d_col_block || !d_col_root_slots || !d_row_subtree_slots || !d_err)
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_split_cols(static_cast<uint8_t*>(d_col_block), k, n_cols, col0,
                                     static_cast<uint8_t*>(d_col_root_slots), static_cast<uint8_t*>(d_row_subtree_slots),
                                     d_err, s);
@@ -189,7 +189,7 @@ int cda_split_combine(cda_ctx* ctx, const void* d_row_subtree_slots, uint32_t pa
     return guarded(ctx, [&](cda::Engine& e) -> int {
         if (!d_row_subtree_slots || !d_col_root_slots || !d_row_roots || !d_col_roots || !d_data_root)
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : e.stream();
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_split_combine(static_cast<const uint8_t*>(d_row_subtree_slots), parts, k,
                                        static_cast<const uint8_t*>(d_col_root_slots),
                                        static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),

@@ -81,7 +81,7 @@ hipError_t launch_row_order(const CellGrid& g, uint32_t n_squares, uint32_t* err
 // One level halves every tree: parent p of tree t goes to
 //   out + y*out_sq + (t*n_in/2 + p)*96;
 // when n_in == 2 the tree roots are written instead as packed 90-B nodes to
-// roots + y*roots_sq + (root0 + t)*90 (if roots) and as 96-B slots to
+// roots + y*roots_sq + t*90 (if roots) and as 96-B slots to
 // root_slots + y*rslot_sq + (root0 + t)*96 (if root_slots).
 struct Forest {
     const uint8_t* in;

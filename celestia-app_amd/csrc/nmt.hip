@@ -201,7 +201,7 @@ __global__ __launch_bounds__(256) void level_kernel(const Forest2 fs, uint32_t n
     inner_node_words(L, R, st.h, o);
     if (n_out == 1) {
         if (F.roots) {
-            uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)(F.root0 + t) * kNode);
+            uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
 #pragma unroll
             for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
         }

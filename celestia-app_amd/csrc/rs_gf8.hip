@@ -131,7 +131,7 @@ constexpr int waves_per_simd() { return K >= 128 ? 2 : 4; }
 
 // Segment of codeword blockIdx.x (uniform) -> byte offsets.
 struct SegSel {
-    uint32_t s0, ss, d0, ds, c0;
+    uint32_t s0, ss, d0, ds, c0, cs;
 };
 __device__ __forceinline__ SegSel select_seg(const RsJob& j, uint32_t cw) {
     const RsSeg& g = (j.n_seg > 1 && cw >= j.seg[0].n_cw) ? j.seg[1] : j.seg[0];
@@ -142,12 +142,12 @@ __device__ __forceinline__ SegSel select_seg(const RsJob& j, uint32_t cw) {
     r.d0 = g.dst_off + c * g.dst_cw;
     r.ds = g.dst_sh;
     r.c0 = g.cpy_off == kNoCopy ? kNoCopy : g.cpy_off + c * g.cpy_cw;
+    r.cs = g.cpy_sh;
     return r;
 }
 
 template <int K>
 __global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_job_kernel(const RsJob job) {
-    constexpr uint32_t SH = 512;
     const SegSel q = select_seg(job, blockIdx.x);
     // Uniform base pointers + 32-bit byte offsets (saddr addressing).
     const uint8_t* src = job.src + blockIdx.y * job.src_sq;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_job_kernel(const
     for (int i = 0; i < K; i++) v[i] = *reinterpret_cast<const uint32_t*>(src + (q.s0 + i * q.ss + lane4));
     if (q.c0 != kNoCopy) {
 #pragma unroll
-        for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(dst + (q.c0 + i * SH + lane4)) = v[i];
+        for (int i = 0; i < K; i++) *reinterpret_cast<uint32_t*>(dst + (q.c0 + i * q.cs + lane4)) = v[i];
     }
     encode_regs<K>(v);
 #pragma unroll

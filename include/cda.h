@@ -96,7 +96,9 @@ int cda_extend_dah_batch(cda_ctx *ctx, const uint8_t *ods, uint32_t k, uint32_t 
                          uint8_t *col_roots, uint8_t *data_roots, int32_t *status);
 
 /* Device-resident batch: every pointer is device memory on ctx's device;
- * stream is a hipStream_t (NULL = the context's stream). Asynchronous: the
+ * stream is a hipStream_t; NULL is HIP's default (null) stream, the one a
+ * PyTorch/Go caller enqueues on by default -- NOT the context's private
+ * stream, so the call is ordered after the caller's own work. Asynchronous: the
  * call only enqueues work. Per-square push-order status is written to d_status
  * (n int32, device memory, may be NULL). */
 int cda_extend_dah_device(cda_ctx *ctx, const void *d_ods, uint32_t k, uint32_t n, void *d_eds, void *d_row_roots,
@@ -118,7 +120,8 @@ int cda_push_order_detail(cda_ctx *ctx, int32_t *axis, uint32_t *index, uint32_t
 
 /* Config 5: ONE square split across G ranks (one GPU each), row blocks +
  * column blocks.  k = ODS width, W = 2k, R = k/G rows and C = W/G columns per
- * rank.  All pointers are device memory; calls only enqueue on `stream`.
+ * rank.  All pointers are device memory; calls only enqueue on `stream`
+ * (NULL = HIP's default stream, as for cda_extend_dah_device).
  * d_err is one uint32 per rank, initialised by the caller to 0xFFFFFFFF;
  * push-order violations atomically lower it (encoding: axis<<24 | index<<12 |
  * position, reduce with MIN across ranks).

@@ -152,9 +152,10 @@ def test_split_square_loopback_on_gpu(ctx, k, parts):
     torch.cuda.synchronize()
     e_eds, e_rows, e_cols, e_root = coracle.cpu_baseline(ods, 16) if k >= 64 else coracle.extend_dah(ods)
     assert int(err.item()) == 0xFFFFFFFF
-    assert root.cpu().numpy().tobytes() == e_root
-    assert np.array_equal(rows.cpu().numpy(), e_rows) and np.array_equal(cols.cpu().numpy(), e_cols)
     assert np.array_equal(cols_eds.cpu().numpy().reshape(-1, 512), e_eds)
+    assert np.array_equal(cols.cpu().numpy(), e_cols)
+    assert np.array_equal(rows.cpu().numpy(), e_rows)
+    assert root.cpu().numpy().tobytes() == e_root
 
 
 def test_split_push_order_on_gpu(ctx):
