@@ -6,7 +6,9 @@ raises, there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import importlib.util
 import os
+import sys
 import threading
 
 import numpy as np
@@ -57,6 +59,12 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
+        # One HIP runtime per process: PyTorch-ROCm bundles its own
+        # libamdhip64 (same soname).  If libcda.so were loaded first, a later
+        # `import torch` would map a second runtime and see no GPU; importing
+        # torch first makes libcda bind to torch's copy.
+        if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
+            import torch  # noqa: F401
         if not os.path.exists(LIB_PATH):
             raise OSError(f"libcda.so not built at {LIB_PATH}; run __graft_entry__.build() "
                           "(no CPU fallback exists)")

@@ -27,6 +27,19 @@ namespace {
 
 constexpr size_t SH = 512;
 
+// Tuning knobs (override with -D).  Measured on MI355X (profiles/r01_sha_sweep.txt):
+// the SHA kernels are VALU-issue-bound; 3-5 waves/SIMD run within 1 %, more
+// waves (forced spills or no prefetch) and non-temporal loads are slower.
+#ifndef CDA_LEAF_WAVES
+#define CDA_LEAF_WAVES 4
+#endif
+#ifndef CDA_LEVEL_WAVES
+#define CDA_LEVEL_WAVES 4
+#endif
+#ifndef CDA_LEAF_PREFETCH
+#define CDA_LEAF_PREFETCH 1
+#endif
+
 __device__ __forceinline__ void load_chunk(const uint4* p, uint32_t (&w)[16]) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -87,9 +100,24 @@ __global__ __launch_bounds__(256) void row_order_kernel(const CellGrid g, uint32
 
 // ---------------------------------------------------------------------------
 // Leaf hashing: one thread per EDS cell, 9 SHA-256 blocks of
-// 0x00 || ns || share, share streamed in 64-B chunks (prefetch one ahead).
+// 0x00 || ns || share.  The share is streamed in 64-B chunks of raw
+// little-endian words; every big-endian message word is ONE v_perm_b32 of two
+// raw words (byte swap and the 30-byte message offset folded together).  Only
+// the upper half of the previous chunk (8 words) is carried between blocks, so
+// the kernel stays under 96 VGPRs (5+ waves per SIMD to hide the dependent
+// SHA round chain).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void leaf_kernel(const CellGrid g, uint8_t* __restrict__ slots,
+__device__ __forceinline__ void load_raw16(const uint4* p, uint32_t (&w)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 v = p[q];
+        w[4 * q + 0] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+}
+// Big-endian message word from share bytes 4j+2 .. 4j+5 (raw words j, j+1).
+__device__ __forceinline__ uint32_t body_word(uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x02030405u); }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEAF_WAVES))) void leaf_kernel(const CellGrid g, uint8_t* __restrict__ slots,
                                                   uint32_t* __restrict__ err, int check_rows, int check_cols) {
     const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
     if (cell >= g.rows * g.cols) return;
@@ -98,63 +126,85 @@ __global__ __launch_bounds__(256) void leaf_kernel(const CellGrid g, uint8_t* __
     const uint32_t gr = g.row0 + r, gc = g.col0 + c, k = g.k;
     const bool parity = !(gr < k && gc < k);
     const uint8_t* E = g.base + sq * g.sq;
-    const uint4* src = reinterpret_cast<const uint4*>(E + ((size_t)r * g.row_stride + c) * SH);
+    const uint8_t* cellp = E + ((size_t)r * g.row_stride + c) * SH;
+    const uint4* src = reinterpret_cast<const uint4*>(cellp);
 
     ShaState st;
     sha_init(st);
-    uint32_t prev[16], cur[16], nxt[16], w[16], nsw[8];
-    load_chunk(src, cur);
-    load_chunk(src + 4, nxt);
-    bswap16(cur);
+    uint32_t cur[16], tail[8], w[16];
+    load_raw16(src, cur);
+#if CDA_LEAF_PREFETCH
+    uint32_t nxt[16];
+    load_raw16(src + 4, nxt);
+#endif
+    // block 0: 0x00 || ns(29) || share[0:34]
+    if (parity) {
+        w[0] = 0x00FFFFFFu;
 #pragma unroll
-    for (int i = 0; i < 8; i++) nsw[i] = parity ? 0xFFFFFFFFu : cur[i];
+        for (int i = 1; i < 7; i++) w[i] = 0xFFFFFFFFu;
+        w[7] = __builtin_amdgcn_perm(cur[0], cur[0], 0x0D0D0001u);
+    } else {
+        w[0] = __builtin_amdgcn_perm(cur[0], cur[0], 0x0C000102u);
 #pragma unroll
-    for (int i = 0; i < 8; i++) w[i] = leaf_msg_head(cur, parity, i);
+        for (int i = 1; i < 7; i++) w[i] = __builtin_amdgcn_perm(cur[i], cur[i - 1], 0x03040506u);
+        w[7] = __builtin_amdgcn_perm(cur[7], cur[6], 0x03040C0Cu) | __builtin_amdgcn_perm(cur[0], cur[0], 0x0C0C0001u);
+    }
 #pragma unroll
-    for (int i = 8; i < 16; i++) w[i] = leaf_msg_body(cur[i - 8], cur[i - 7]);
+    for (int i = 8; i < 16; i++) w[i] = body_word(cur[i - 8], cur[i - 7]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) tail[i] = cur[8 + i];
     sha_compress(st, w);
 
 #pragma unroll 1
     for (int b = 1; b < 8; b++) {
+#if CDA_LEAF_PREFETCH
 #pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = cur[i];
+        for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+        if (b < 7) load_raw16(src + 4 * (b + 1), nxt);
+#else
+        load_raw16(src + 4 * b, cur);
+#endif
 #pragma unroll
-        for (int i = 0; i < 16; i++) cur[i] = bswap32(nxt[i]);
-        if (b < 7) load_chunk(src + 4 * (b + 1), nxt);
+        for (int t = 0; t < 7; t++) w[t] = body_word(tail[t], tail[t + 1]);
+        w[7] = body_word(tail[7], cur[0]);
 #pragma unroll
-        for (int t = 0; t < 7; t++) w[t] = leaf_msg_body(prev[8 + t], prev[9 + t]);
-        w[7] = leaf_msg_body(prev[15], cur[0]);
+        for (int t = 8; t < 16; t++) w[t] = body_word(cur[t - 8], cur[t - 7]);
 #pragma unroll
-        for (int t = 8; t < 16; t++) w[t] = leaf_msg_body(cur[t - 8], cur[t - 7]);
+        for (int i = 0; i < 8; i++) tail[i] = cur[8 + i];
         sha_compress(st, w);
     }
-    // block 8: share words 120..127 then padding
+    // block 8: share words 120..127 then padding (542-B message)
 #pragma unroll
-    for (int t = 0; t < 7; t++) w[t] = leaf_msg_body(cur[8 + t], cur[9 + t]);
-    w[7] = (cur[15] << 16) | 0x8000u;
+    for (int t = 0; t < 7; t++) w[t] = body_word(tail[t], tail[t + 1]);
+    w[7] = __builtin_amdgcn_perm(tail[7], tail[7], 0x02030C0Cu) | 0x8000u;
 #pragma unroll
     for (int t = 8; t < 15; t++) w[t] = 0;
     w[15] = kLeafMsgBits;
     sha_compress(st, w);
 
+    // namespace (big-endian words) reloaded: L2/MALL-hot, saves 8 live VGPRs
+    uint32_t nsw[8];
+    if (parity) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nsw[i] = 0xFFFFFFFFu;
+    } else {
+        load_ns_be(cellp, nsw);
+    }
     uint32_t out[kSlotWords];
     leaf_node_words(nsw, st.h, out);
     store_slot(slots + (sq * (size_t)g.rows * g.cols + cell) * kSlot, out);
 
     // nmt push-order check of Q0 (fused: this cell's namespace is in nsw)
     if (!parity) {
-        uint32_t me[8], nb[8];
-#pragma unroll
-        for (int i = 0; i < 7; i++) me[i] = nsw[i];
-        me[7] = nsw[7] & 0xFF000000u;
+        uint32_t nb[8];
         uint32_t key = 0xFFFFFFFFu;
         if (check_rows && gc + 1 < k && c + 1 < g.cols) {
-            load_ns_be(E + ((size_t)r * g.row_stride + c + 1) * SH, nb);
-            if (ns_less(nb, me)) key = min(key, (0u << 24) | (gr << 12) | (gc + 1));
+            load_ns_be(cellp + SH, nb);
+            if (ns_less(nb, nsw)) key = min(key, (0u << 24) | (gr << 12) | (gc + 1));
         }
         if (check_cols && gr + 1 < k && r + 1 < g.rows) {
-            load_ns_be(E + ((size_t)(r + 1) * g.row_stride + c) * SH, nb);
-            if (ns_less(nb, me)) key = min(key, (1u << 24) | (gc << 12) | (gr + 1));
+            load_ns_be(cellp + (size_t)g.row_stride * SH, nb);
+            if (ns_less(nb, nsw)) key = min(key, (1u << 24) | (gc << 12) | (gr + 1));
         }
         if (key != 0xFFFFFFFFu) atomicMin(err + sq, key);
     }
@@ -171,7 +221,7 @@ struct Forest2 {
     Forest f[2];
 };
 
-__global__ __launch_bounds__(256) void level_kernel(const Forest2 fs, uint32_t n_in) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_WAVES))) void level_kernel(const Forest2 fs, uint32_t n_in) {
     const Forest& F = fs.f[blockIdx.z];
     const uint32_t n_out = n_in / 2;
     const uint32_t idx = blockIdx.x * 256 + threadIdx.x;

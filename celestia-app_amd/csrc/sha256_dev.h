@@ -90,6 +90,7 @@ CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
     s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
 
+
 // ---------------------------------------------------------------------------
 // Leaf: message word i (big-endian) of 0x00 || ns || share, given the share as
 // big-endian words S[0..127] and `parity` (ns = 0xFF*29 instead of share[0:29]).
