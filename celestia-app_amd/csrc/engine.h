@@ -94,6 +94,15 @@ class Engine {
 
     int device_;
     hipStream_t stream_ = nullptr;
+    // Batch pipeline: RS of chunk i+1 (HBM/VALU mix) overlaps the SHA-256
+    // stages of chunk i (VALU) on a second stream.
+    hipStream_t rs_stream_ = nullptr, hash_stream_ = nullptr;
+    std::vector<hipEvent_t> sync_events_;
+    uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
+    hipEvent_t sync_event(size_t i);
+    int enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
+                                  uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
+                                  hipStream_t s);
     std::mutex mu_;
     std::string err_;
     DevBuf gf16_log_, gf16_exp_, gf16_skew_;

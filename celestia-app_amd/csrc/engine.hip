@@ -10,6 +10,7 @@
 #include "engine.h"
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -53,7 +54,10 @@ Engine::~Engine() {
         if (m.b) (void)hipEventDestroy(m.b);
     }
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
+    for (hipEvent_t e : sync_events_) (void)hipEventDestroy(e);
     if (stream_) (void)hipStreamDestroy(stream_);
+    if (rs_stream_) (void)hipStreamDestroy(rs_stream_);
+    if (hash_stream_) (void)hipStreamDestroy(hash_stream_);
 }
 
 int Engine::check(hipError_t e, const char* what) {
@@ -74,6 +78,9 @@ int Engine::init() {
     int rc;
     if ((rc = check(hipSetDevice(device_), "hipSetDevice"))) return rc;
     if ((rc = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if ((rc = check(hipStreamCreateWithFlags(&rs_stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if ((rc = check(hipStreamCreateWithFlags(&hash_stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -304,12 +311,65 @@ int Engine::enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint
     return check(launch_data_root(rs, 2 * W, 1, d_root, s), "data root");
 }
 
-int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
-                               uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
-                               hipStream_t s) {
+int Engine::enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds,
+                                      uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err,
+                                      int32_t* d_status, hipStream_t s) {
     int rc = enqueue_extend(d_ods, k, n, d_eds, s);
     if (rc) return rc;
     return enqueue_dah(d_eds, k, n, d_rows, d_cols, d_roots, d_err, d_status, s);
+}
+
+hipEvent_t Engine::sync_event(size_t i) {
+    while (sync_events_.size() <= i) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+        sync_events_.push_back(e);
+    }
+    return sync_events_[i];
+}
+
+// Batch pipeline.  The batch is cut into chunks of c squares; chunk i's RS
+// extension runs on rs_stream_, its roots on hash_stream_ after an event, so
+// the RS of chunk i+1 (memory-heavy) overlaps the SHA-256 of chunk i
+// (VALU-bound).  Both internal streams start after the work already queued on
+// the caller's stream `s`, and `s` waits for both at the end, so the call keeps
+// single-stream semantics for the caller.  Events are re-recorded by later
+// calls only after hipStreamWaitEvent has captured them (HIP semantics).
+int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
+                               uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
+                               hipStream_t s) {
+    if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
+    // Default serial: measured on MI355X (profiles/r01_pipeline_sweep.txt) the
+    // v_perm GF(2^8) encoder is VALU-bound like SHA-256, so co-running them
+    // only shares the SIMDs (and per-chunk level/data-root tails cost extra).
+    uint32_t c = pipeline_chunk_ ? pipeline_chunk_ : n;
+    if (c >= n) return enqueue_extend_dah_serial(d_ods, k, n, d_eds, d_rows, d_cols, d_roots, d_err, d_status, s);
+    const uint32_t W = 2 * k;
+    const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = (uint64_t)W * W * kShare;
+    const uint32_t n_chunks = (n + c - 1) / c;
+    int rc;
+    hipEvent_t start = sync_event(0);
+    if (!start || !sync_event(n_chunks + 2)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
+    if ((rc = check(hipEventRecord(start, s), "hipEventRecord"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(rs_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(hash_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
+    for (uint32_t i = 0; i < n_chunks; i++) {
+        const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
+        uint8_t* eds = d_eds + i0 * eds_sq;
+        if ((rc = enqueue_extend(d_ods + i0 * ods_sq, k, m, eds, rs_stream_))) return rc;
+        hipEvent_t ev = sync_event(1 + i);
+        if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(hash_stream_, ev, 0), "hipStreamWaitEvent"))) return rc;
+        if ((rc = enqueue_dah(eds, k, m, d_rows + (size_t)i0 * W * kNode, d_cols + (size_t)i0 * W * kNode,
+                              d_roots + (size_t)i0 * 32, d_err + i0, d_status ? d_status + i0 : nullptr,
+                              hash_stream_)))
+            return rc;
+    }
+    hipEvent_t done = sync_event(1 + n_chunks);
+    if ((rc = check(hipEventRecord(done, hash_stream_), "hipEventRecord"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent"))) return rc;
+    // rs_stream_ work all precedes `done` through the per-chunk events.
+    return CDA_OK;
 }
 
 int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n,
