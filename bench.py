@@ -105,6 +105,55 @@ def cpu_baseline(k: int, seconds: float, threads: int):
                       f"amd64 assembly; {threads} host threads, {el:.1f}s)"}
 
 
+def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
+    """Config 5 timing: one k x k square split over `world`
+    GPUs.  Returns ms per square (max over ranks) and the data root; rank 0
+    also checks it against its single-GPU extend_dah of the same square."""
+    import torch
+    import torch.distributed as dist
+
+    from celestia_da import dist as cdist
+    from celestia_da import testfactory
+
+    ods = testfactory.random_square(k, 0).reshape(k, k, SHARE)
+    R = k // world
+    mine = torch.from_numpy(ods[rank * R:(rank + 1) * R].copy()).to(dev)
+    ops = cdist.GpuSplitOps(ctx, dev)
+    errors = []
+    # every rank runs the same collectives even if a local step fails
+    res = cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append)          # warm-up
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        res = cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0, float(len(errors))], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if el[1].item() > 0:
+        return {"error": repr(errors[0]) if errors else "failed on another rank"}
+    out = {"k": k, "gpus": world, "ms_per_square": 1e3 * float(el[0].item()) / iters,
+           "squares_per_s": iters / float(el[0].item()),
+           "all_to_all_bytes_per_rank": (k // world) * (2 * k) * SHARE * (world - 1) // world}
+    if rank == 0:
+        rows, cols, root, err = res[2]
+        out["data_root"] = root.cpu().numpy().tobytes().hex()
+        W = 2 * k
+        e = torch.empty(W * W * SHARE, dtype=torch.uint8, device=dev)
+        r1 = torch.empty(W * 90, dtype=torch.uint8, device=dev)
+        c1 = torch.empty(W * 90, dtype=torch.uint8, device=dev)
+        g1 = torch.empty(32, dtype=torch.uint8, device=dev)
+        o = torch.from_numpy(ods.reshape(-1, SHARE).copy()).to(dev)
+        ctx.extend_dah_device(o.data_ptr(), k, 1, e.data_ptr(), r1.data_ptr(), c1.data_ptr(), g1.data_ptr(),
+                              None, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        out["matches_single_gpu"] = bool(torch.equal(g1, root) and torch.equal(r1.view(W, 90), rows)
+                                         and torch.equal(c1.view(W, 90), cols) and int(err.item()) == 0xFFFFFFFF)
+        del e
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,6 +282,15 @@ def main():
                           "ods_gb_per_s": n5 * k5 * k5 * SHARE / el5 / 1e9,
                           "data_root": g5.cpu().numpy().tobytes().hex(),
                           "stages": stage_report(ctx.stage_times(), k5, 1)}
+
+    if world > 1 and not args.no_extras:
+        # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
+        # all-to-all of the row-encoded blocks, column encode + hashing per
+        # rank, gather of subtree/column roots, combine on rank 0).
+        try:
+            extras["config5"] = config5(ctx, dev, rank, world, 512)
+        except Exception as e:  # report, never lose the headline line
+            extras["config5"] = {"error": f"{type(e).__name__}: {e}"}
 
     cpu = None
     if rank == 0 and not args.no_cpu:

@@ -72,11 +72,16 @@ class GpuSplitOps:
         return rows, cols, root
 
 
-def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None):
+def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None, on_error=None):
     """Config 5 on this rank.  `ods_rows` = this rank's R x k ODS shares
     (tensor on the rank's device).  Returns (row_block, col_block, result)
     where result = (row_roots, col_roots, data_root, err_word) on rank 0 and
-    None elsewhere.  err_word is the MIN over ranks (0xFFFFFFFF = ordered)."""
+    None elsewhere.  err_word is the MIN over ranks (0xFFFFFFFF = ordered).
+
+    on_error: if given, a failing LOCAL step calls on_error(exc) and the rank
+    carries on with placeholder tensors, so every rank still enters every
+    collective in the same order (a raise on one rank would leave the others
+    blocked in the all-to-all or the gathers)."""
     import torch
     import torch.distributed as dist
 
@@ -84,8 +89,19 @@ def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None):
     if k % world or W % world:
         raise ValueError("world size must divide k")
     R, C = k // world, W // world
+
+    def local(fn, fallback):
+        if on_error is None:
+            return fn()
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported through on_error
+            on_error(e)
+            return fallback()
+
     err = ops.new_err()
-    rb = ops.rows(ods_rows, k, rank * R, err)                                   # [R][W][512]
+    rb = local(lambda: ops.rows(ods_rows, k, rank * R, err),
+               lambda: torch.zeros((R, W, SHARE), dtype=torch.uint8, device=ods_rows.device))  # [R][W][512]
     send = rb.view(R, world, C, SHARE).permute(1, 0, 2, 3).contiguous()        # [dst][R][C][512]
     recv = torch.empty_like(send)                                               # [src][R][C][512]
     if world > 1:
@@ -94,7 +110,9 @@ def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None):
         recv.copy_(send)
     block = torch.empty((W, C, SHARE), dtype=torch.uint8, device=rb.device)
     block[:k] = recv.reshape(k, C, SHARE)                                       # rows 0..k-1 of my columns
-    col_slots, row_sub = ops.cols(block, k, rank * C, err)
+    col_slots, row_sub = local(lambda: ops.cols(block, k, rank * C, err),
+                               lambda: (torch.zeros((C, SLOT), dtype=torch.uint8, device=rb.device),
+                                        torch.zeros((W, SLOT), dtype=torch.uint8, device=rb.device)))
     err = err.to(torch.int64) & 0xFFFFFFFF          # the kernels' uint32 word; MIN needs unsigned order
     if world > 1:
         dist.all_reduce(err, op=dist.ReduceOp.MIN, group=group)
@@ -109,8 +127,8 @@ def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None):
     if rank == 0:
         row_sub_all = torch.stack(rs).contiguous()                              # [G][W][96]
         col_all = torch.cat(cs).contiguous()                                    # [W][96]
-        rows, cols, root = ops.combine(row_sub_all, world, k, col_all)
-        result = (rows, cols, root, err)
+        combined = local(lambda: ops.combine(row_sub_all, world, k, col_all), lambda: None)
+        result = None if combined is None else (*combined, err)
     return rb, block, result
 
 
