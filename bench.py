@@ -129,7 +129,8 @@ def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
         res = cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append)
     torch.cuda.synchronize(dev)
     dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0, float(len(errors))], dtype=torch.float64, device=dev)
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    el = torch.tensor([time.perf_counter() - t0, float(len(errors))], dtype=torch.float64, device=on)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if el[1].item() > 0:
         return {"error": repr(errors[0]) if errors else "failed on another rank"}

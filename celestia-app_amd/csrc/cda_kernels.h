@@ -100,6 +100,14 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
 // RFC-6962 data root over n_items 96-B root slots per square (power of two).
 hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares, uint8_t* data_roots,
                             hipStream_t stream);
+// The same from the root slots in two wide launches: RFC-6962 leaf digests
+// (one thread per root, into `digests`: n_items*n_squares*32 B of scratch),
+// then one workgroup per square for the inner levels (n_items a power of two
+// <= 4096).
+hipError_t launch_data_root_slots(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares,
+                                  uint32_t* digests, uint8_t* data_roots, hipStream_t stream);
+hipError_t launch_data_root_digests(const uint32_t* digests, uint32_t n_items, uint32_t n_squares,
+                                    uint8_t* data_roots, hipStream_t stream);
 // Pack n_slots 96-B root slots (rows then columns) into 90-B roots.
 hipError_t launch_slots_to_roots(const uint8_t* slots, uint32_t n_slots, uint8_t* rows, uint8_t* cols, uint32_t w,
                                  hipStream_t stream);

@@ -46,7 +46,7 @@ Engine::Engine(int device) : device_(device) {}
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
     for (DevBuf* b : {&gf16_chunk_[0], &gf16_chunk_[1], &gf16_log_, &gf16_exp_,
-                      &gf16_skew_, &leaf_, &lvl_, &root_slots_, &err_buf_, &h_ods_, &h_eds_,
+                      &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &h_ods_, &h_eds_,
                       &h_rows_, &h_cols_, &h_roots_})
         b->release();
     for (Mark& m : marks_) {
@@ -224,6 +224,8 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     mark_begin(kStageLevels, s);
     // row trees: leaves (t, i); column trees: leaves (i, t) of the same leaf grid
     Forest f[2]{};
+    // roots go packed to d_rows / d_cols and as 96-B slots (rows then
+    // columns) to root_slots_ for the data root
     f[0] = Forest{leaf_.as<uint8_t>(), slots_sq, W, W, 1, nullptr, 0, d_rows, (uint64_t)W * kNode,
                   root_slots_.as<uint8_t>(), (uint64_t)2 * W * kSlot, 0};
     f[1] = Forest{leaf_.as<uint8_t>(), slots_sq, W, 1, W, nullptr, 0, d_cols, (uint64_t)W * kNode,
@@ -232,7 +234,10 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     if ((rc = run_forests(f, 2, W, n, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), slots_sq, off, s))) return rc;
     mark_end(s);
     mark_begin(kStageDataRoot, s);
-    if ((rc = check(launch_data_root(root_slots_.as<uint8_t>(), 2 * W, n, d_roots, s), "data root"))) return rc;
+    if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
+    if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s),
+                    "data root")))
+        return rc;
     mark_end(s);
     if (d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
     return CDA_OK;

@@ -312,6 +312,67 @@ __global__ __launch_bounds__(256) void data_root_kernel(const uint8_t* __restric
     }
 }
 
+// RFC-6962 leaf digests sha256(0x00 || root) of n 96-B root slots (one thread
+// each, 2 compressions), 8 big-endian-valued words per digest.
+__global__ __launch_bounds__(256) void rfc_leaf_kernel(const uint8_t* __restrict__ slots, uint32_t n,
+                                                      uint32_t* __restrict__ dig) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t I[kSlotWords], w[16];
+    load_slot_be(slots + (size_t)i * kSlot, I);
+    ShaState st;
+    sha_init(st);
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
+        sha_compress(st, w);
+    }
+    uint4* d = reinterpret_cast<uint4*>(dig + (size_t)i * 8);
+    d[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+    d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+}
+
+// Data root from the 2W leaf digests (rfc_leaf_kernel): one
+// workgroup per square, n/2 threads (<= 1024) hash the first inner level
+// straight from global memory, later levels ping-pong in LDS.
+__global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
+                                                               uint8_t* __restrict__ data_roots) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [n/2][8] | [n/4][8]
+    const size_t sq = blockIdx.x;
+    const uint32_t* D = dig + sq * (size_t)n * 8;
+    uint32_t* src = hs;
+    uint32_t* dst = hs + (n / 2) * 8;
+    for (uint32_t m = n / 2; m >= 1; m >>= 1) {
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            uint32_t A[8], B[8], w[16];
+            const uint32_t* a = m == n / 2 ? D + (2 * i) * 8 : src + (2 * i) * 8;
+#pragma unroll
+            for (int j = 0; j < 8; j++) { A[j] = a[j]; B[j] = a[8 + j]; }
+            ShaState st;
+            sha_init(st);
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(A, B, 16 * b + j);
+                sha_compress(st, w);
+            }
+            uint32_t* o = m == n / 2 ? src + i * 8 : dst + i * 8;
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = st.h[j];
+        }
+        __syncthreads();
+        if (m != n / 2) {
+            uint32_t* t = src; src = dst; dst = t;
+        }
+    }
+    if (threadIdx.x == 0) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(data_roots + sq * 32);
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = bswap32(src[j]);
+    }
+}
+
 __global__ void status_kernel(const uint32_t* __restrict__ err, uint32_t n, int32_t* __restrict__ status) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) status[i] = err[i] == 0xFFFFFFFFu ? 0 : -3;   // CDA_OK / CDA_ERR_PUSH_ORDER
@@ -378,6 +439,30 @@ hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(data_root_kernel, dim3(n), dim3(256), lds, s, root_slots, n_items, data_roots);
+    return hipGetLastError();
+}
+
+hipError_t launch_data_root_slots(const uint8_t* root_slots, uint32_t n_items, uint32_t n, uint32_t* dig,
+                                  uint8_t* data_roots, hipStream_t s) {
+    if (n_items < 2 || n_items > 4096 || (n_items & (n_items - 1))) return hipErrorInvalidValue;
+    const uint32_t total = n_items * n;
+    hipLaunchKernelGGL(rfc_leaf_kernel, dim3((total + 255) / 256), dim3(256), 0, s, root_slots, total, dig);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_data_root_digests(dig, n_items, n, data_roots, s);
+}
+
+hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint32_t n, uint8_t* data_roots,
+                                    hipStream_t s) {
+    if (n_items < 2 || n_items > 4096 || (n_items & (n_items - 1))) return hipErrorInvalidValue;
+    const size_t lds = (size_t)(n_items / 2 + n_items / 4) * 32;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(data_root_digest_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t threads = n_items / 2 < 1024 ? (n_items / 2 < 64 ? 64 : n_items / 2) : 1024;
+    hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots);
     return hipGetLastError();
 }
 

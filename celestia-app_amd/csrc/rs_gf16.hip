@@ -16,8 +16,10 @@
 //   pass B : wave w holds the shards of R = S/16 residues r (r + S*t,
 //            t = 0..15) and runs IFFT d = S..k/2 then FFT d = k/2..S;
 //   pass A': FFT layers d < S, write parity.
-// The two layout changes go through the codeword's own parity region
-// (L2/MALL resident) with a workgroup barrier; no LDS.
+// The whole codeword stays in the workgroup's registers; the two layout
+// changes are register all-to-alls between the 16 waves through 128 KiB of
+// LDS (R rounds each way), so HBM sees only the data read, the optional Q0
+// copy and the parity write.
 //
 // Multiply by a constant c: y is split into 2-bit chunks (four per byte); each
 // chunk selects one of 4 bytes of a table dword with v_perm_b32(T, T, sel),
@@ -135,8 +137,11 @@ __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], c
     });
 }
 
+constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
+
 template <int K>
 __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const RsJob job) {
+    extern __shared__ uint32_t X[];
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
     const Tab16 T{tab};
@@ -171,37 +176,70 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         *reinterpret_cast<uint32_t*>(base + a + 32) = h;
     };
 
+    // The whole codeword (K shards x 512 B = 256 KiB at K = 512) stays in the
+    // workgroup's registers: 2S dwords per lane.  The layout changes between
+    // the passes go through 128 KiB of LDS in R rounds; round q moves the
+    // registers j = R*jj + q (jj = 0..15) of every wave t to wave jj, where
+    // they become residue R*jj + q's shard t -- in place, so pass B's
+    // residue q lives in registers {R*t + q}.
+    uint32_t lo[S], hi[S];
+    auto xchg_a_to_b = [&]() {
+        sfor<0, R, 1>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            if (q) __syncthreads();
+            sfor<0, 16, 1>([&](auto jj) {
+                constexpr int j = R * decltype(jj)::value + q;
+                X[((wave * 16 + jj.value) * 2 + 0) * 64 + lane] = lo[j];
+                X[((wave * 16 + jj.value) * 2 + 1) * 64 + lane] = hi[j];
+            });
+            __syncthreads();
+            sfor<0, 16, 1>([&](auto tt) {
+                constexpr int j = R * decltype(tt)::value + q;
+                lo[j] = X[((tt.value * 16 + wave) * 2 + 0) * 64 + lane];
+                hi[j] = X[((tt.value * 16 + wave) * 2 + 1) * 64 + lane];
+            });
+        });
+    };
+    auto xchg_b_to_a = [&]() {
+        sfor<0, R, 1>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            __syncthreads();
+            sfor<0, 16, 1>([&](auto tt) {
+                constexpr int j = R * decltype(tt)::value + q;
+                X[((tt.value * 16 + wave) * 2 + 0) * 64 + lane] = lo[j];
+                X[((tt.value * 16 + wave) * 2 + 1) * 64 + lane] = hi[j];
+            });
+            __syncthreads();
+            sfor<0, 16, 1>([&](auto jj) {
+                constexpr int j = R * decltype(jj)::value + q;
+                lo[j] = X[((wave * 16 + jj.value) * 2 + 0) * 64 + lane];
+                hi[j] = X[((wave * 16 + jj.value) * 2 + 1) * 64 + lane];
+            });
+        });
+    };
+
     // ---------------- pass A: IFFT d = 1 .. S/2 -------------------------
-    {
-        uint32_t lo[S], hi[S];
-        const uint32_t base = S * wave;
-        sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (base + jj.value) * ss, lo[jj.value], hi[jj.value]); });
-        if (c0 != kNoCopy) {
-            sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * g.cpy_sh, lo[jj.value], hi[jj.value]); });
-        }
-        ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + base; });
-        sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
+    const uint32_t base = S * wave;
+    sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (base + jj.value) * ss, lo[jj.value], hi[jj.value]); });
+    if (c0 != kNoCopy) {
+        sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * g.cpy_sh, lo[jj.value], hi[jj.value]); });
     }
-    __syncthreads();
+    ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + base; });
+    xchg_a_to_b();
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
-    sfor<0, R, 1>([&](auto rr) {
-        constexpr int r = decltype(rr)::value;
-        uint32_t lo[16], hi[16];
-        const uint32_t b0 = d0 + (R * wave + r) * ds;
-        sfor<0, 16, 1>([&](auto tt) { ld(E, b0 + (S * tt.value) * ds, lo[tt.value], hi[tt.value]); });
-        ifft_regs<16>(lo, hi, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
-        fft_regs<16>(lo, hi, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
-        sfor<0, 16, 1>([&](auto tt) { st(E, b0 + (S * tt.value) * ds, lo[tt.value], hi[tt.value]); });
+    // residue R*wave + q: shards R*wave + q + S*t in registers R*t + q
+    sfor<0, R, 1>([&](auto qq) {
+        constexpr int q = decltype(qq)::value;
+        uint32_t l16[16], h16[16];
+        sfor<0, 16, 1>([&](auto tt) { l16[tt.value] = lo[R * tt.value + q]; h16[tt.value] = hi[R * tt.value + q]; });
+        ifft_regs<16>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
+        fft_regs<16>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
+        sfor<0, 16, 1>([&](auto tt) { lo[R * tt.value + q] = l16[tt.value]; hi[R * tt.value + q] = h16[tt.value]; });
     });
-    __syncthreads();
-    // ---------------- pass A': FFT d = S/2 .. 1 --------------------------
-    {
-        uint32_t lo[S], hi[S];
-        const uint32_t base = S * wave;
-        sfor<0, S, 1>([&](auto jj) { ld(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
-        fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + base; });
-        sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
-    }
+    xchg_b_to_a();
+    // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
+    fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + base; });
+    sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
 }
 
 // ---------------------------------------------------------------------------
@@ -297,7 +335,14 @@ __global__ __launch_bounds__(256) void rs16_flat_kernel(Gf16Dev t, const uint8_t
 template <int K>
 hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s) {
     const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
-    hipLaunchKernelGGL(rs16_cw_kernel<K>, dim3(ncw, n), dim3(1024), 0, s, t.chunk, j);
+    static bool attr = false;   // set once per instantiation (function attribute, all devices)
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs16_cw_kernel<K>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXchgBytes);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(rs16_cw_kernel<K>, dim3(ncw, n), dim3(1024), kXchgBytes, s, t.chunk, j);
     return hipGetLastError();
 }
 
