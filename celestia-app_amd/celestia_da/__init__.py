@@ -1,9 +1,10 @@
 """celestia_da -- MI355X-native celestia-app data-availability hot path.
 
-Host-side mirror of the reference's Go API (pkg/da, pkg/wrapper, rsmt2d) over
-the C ABI of libcda.so (include/cda.h).  See DESIGN.md.
+Host-side mirror of the reference's Go API (pkg/da, pkg/wrapper, rsmt2d,
+go-square square) over the C ABI of libcda.so (include/cda.h).  See DESIGN.md.
 """
-from . import _lib, da, rsmt2d, wrapper  # noqa: F401
-from ._lib import CdaError, Context, PushOrderError, default_context, load  # noqa: F401
+from . import _lib, blobfactory, da, rsmt2d, square, wrapper  # noqa: F401
+from ._lib import CdaError, Context, PushOrderError, SquareError, default_context, load  # noqa: F401
 
-__all__ = ["da", "rsmt2d", "wrapper", "Context", "CdaError", "PushOrderError", "default_context", "load"]
+__all__ = ["da", "rsmt2d", "wrapper", "square", "blobfactory", "Context", "CdaError", "PushOrderError", "SquareError",
+           "default_context", "load"]

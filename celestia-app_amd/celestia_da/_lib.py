@@ -29,12 +29,17 @@ CDA_ERR_DEVICE = -4
 CDA_ERR_OOM = -5
 CDA_ERR_INVALID = -6
 CDA_ERR_UNSUPPORTED = -7
+CDA_ERR_SQUARE = -8
+
+CDA_SQUARE_CONSTRUCT = 0
+CDA_SQUARE_BUILD = 1
 
 EXPORTED = (
     "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
     "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
     "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
+    "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -47,6 +52,10 @@ class CdaError(RuntimeError):
 
 class PushOrderError(CdaError):
     """nmt ErrInvalidPushOrder surfaced through RowRoots/ColRoots."""
+
+
+class SquareError(CdaError):
+    """go-square square.Construct / Build error."""
 
 
 _lib = None
@@ -90,6 +99,16 @@ def load():
         L.cda_split_rows.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.cda_split_cols.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
         L.cda_split_combine.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
+        u32p = C.POINTER(C.c_uint32)
+        u64p = C.POINTER(C.c_uint64)
+        L.cda_square_layout.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, u32p, u32p,
+                                        u32p, u32p, C.c_uint32, u32p]
+        L.cda_square_construct.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, u8p,
+                                           C.c_size_t, u32p, u32p, u32p]
+        L.cda_construct_extend_dah.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, u8p,
+                                               C.c_size_t, u8p, u8p, C.c_size_t, u8p, u32p, u32p, u32p]
+        L.cda_square_construct_device.argtypes = [ctxp, u8p, u64p, C.c_uint32, vp, C.c_uint32, C.c_uint32, C.c_int,
+                                                  vp, C.c_size_t, u32p, u32p, u32p, vp]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L
@@ -131,6 +150,8 @@ class Context:
         msg = self.lib.cda_last_error(self.h).decode()
         if rc == CDA_ERR_PUSH_ORDER:
             raise PushOrderError(rc, msg)
+        if rc == CDA_ERR_SQUARE:
+            raise SquareError(rc, msg)
         raise CdaError(rc, msg)
 
     def set_profiling(self, on: bool):

@@ -46,6 +46,24 @@ int not_pow2(cda::Engine& e, uint32_t n) {
     return e.fail(CDA_ERR_NOT_POW2, buf);
 }
 
+// Last error of context-free calls (cda_square_layout with ctx == NULL).
+thread_local std::string tl_error;
+
+int plan_square(const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs, uint32_t max_square_size,
+                uint32_t threshold, int mode, cda::square::Plan* p, std::string* err) {
+    if (mode != CDA_SQUARE_CONSTRUCT && mode != CDA_SQUARE_BUILD) {
+        *err = "unknown square construction mode";
+        return -1;
+    }
+    for (uint32_t i = 0; i < n_txs; i++)
+        if (tx_off[i + 1] < tx_off[i]) {
+            *err = "tx offsets must be non-decreasing";
+            return -1;
+        }
+    return cda::square::plan(txs, tx_off, n_txs, max_square_size, threshold,
+                             mode == CDA_SQUARE_BUILD ? cda::square::kBuild : cda::square::kConstruct, p, err);
+}
+
 }  // namespace
 
 extern "C" {
@@ -71,7 +89,7 @@ int cda_ctx_destroy(cda_ctx* ctx) {
     return CDA_OK;
 }
 
-const char* cda_last_error(cda_ctx* ctx) { return ctx ? ctx->eng.last_error().c_str() : "null context"; }
+const char* cda_last_error(cda_ctx* ctx) { return ctx ? ctx->eng.last_error().c_str() : tl_error.c_str(); }
 
 int cda_extend_shares(cda_ctx* ctx, const uint8_t* ods, uint32_t n_shares, uint8_t* eds) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
@@ -194,6 +212,114 @@ int cda_split_combine(cda_ctx* ctx, const void* d_row_subtree_slots, uint32_t pa
                                        static_cast<const uint8_t*>(d_col_root_slots),
                                        static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
                                        static_cast<uint8_t*>(d_data_root), s);
+    });
+}
+
+int cda_square_layout(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs,
+                      uint32_t max_square_size, uint32_t threshold, int mode, uint32_t* square_size, uint32_t* kept,
+                      uint32_t* n_kept, uint32_t* share_indexes, uint32_t share_index_cap, uint32_t* n_share_indexes) {
+    // Host-only (no device work): usable without a context.
+    auto run = [&](std::string* err) -> int {
+        if (!square_size || (n_txs && (!txs || !tx_off))) {
+            *err = "null buffer";
+            return CDA_ERR_INVALID;
+        }
+        cda::square::Plan p;
+        if (plan_square(txs, tx_off, n_txs, max_square_size, threshold, mode, &p, err)) return CDA_ERR_SQUARE;
+        *square_size = p.square_size;
+        if (kept) {
+            memcpy(kept, p.kept.data(), p.kept.size() * 4);
+            if (n_kept) *n_kept = (uint32_t)p.kept.size();
+        }
+        if (n_share_indexes) *n_share_indexes = (uint32_t)p.share_indexes.size();
+        if (share_indexes) {
+            if (p.share_indexes.size() > share_index_cap) {
+                *err = "share_indexes capacity too small";
+                return CDA_ERR_INVALID;
+            }
+            memcpy(share_indexes, p.share_indexes.data(), p.share_indexes.size() * 4);
+        }
+        return CDA_OK;
+    };
+    if (!ctx) {
+        tl_error.clear();
+        try {
+            return run(&tl_error);
+        } catch (const std::bad_alloc&) {
+            tl_error = "host allocation failed";
+            return CDA_ERR_OOM;
+        }
+    }
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        std::string err;
+        const int rc = run(&err);
+        return rc ? e.fail(rc, err) : CDA_OK;
+    });
+}
+
+int cda_square_construct(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs,
+                         uint32_t max_square_size, uint32_t threshold, int mode, uint8_t* ods, size_t ods_capacity,
+                         uint32_t* square_size, uint32_t* kept, uint32_t* n_kept) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!ods || !square_size || (n_txs && (!txs || !tx_off))) return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda::square::Plan p;
+        std::string err;
+        if (plan_square(txs, tx_off, n_txs, max_square_size, threshold, mode, &p, &err))
+            return e.fail(CDA_ERR_SQUARE, err);
+        *square_size = p.square_size;
+        if (kept) {
+            memcpy(kept, p.kept.data(), p.kept.size() * 4);
+            if (n_kept) *n_kept = (uint32_t)p.kept.size();
+        }
+        if ((size_t)p.square_size * p.square_size * CDA_SHARE_SIZE > ods_capacity)
+            return e.fail(CDA_ERR_INVALID, "ods capacity too small for the square");
+        return e.host_square(p, txs, n_txs ? tx_off[n_txs] : 0, ods);
+    });
+}
+
+int cda_construct_extend_dah(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs,
+                             uint32_t max_square_size, uint32_t threshold, int mode, uint8_t* eds, size_t eds_capacity,
+                             uint8_t* row_roots, uint8_t* col_roots, size_t roots_capacity, uint8_t* data_root,
+                             uint32_t* square_size, uint32_t* kept, uint32_t* n_kept) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!row_roots || !col_roots || !data_root || !square_size || (n_txs && (!txs || !tx_off)))
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda::square::Plan p;
+        std::string err;
+        if (plan_square(txs, tx_off, n_txs, max_square_size, threshold, mode, &p, &err))
+            return e.fail(CDA_ERR_SQUARE, err);
+        *square_size = p.square_size;
+        if (kept) {
+            memcpy(kept, p.kept.data(), p.kept.size() * 4);
+            if (n_kept) *n_kept = (uint32_t)p.kept.size();
+        }
+        const size_t w = 2 * (size_t)p.square_size;
+        if (w * CDA_NMT_ROOT_SIZE > roots_capacity) return e.fail(CDA_ERR_INVALID, "roots capacity too small");
+        if (eds && w * w * CDA_SHARE_SIZE > eds_capacity) return e.fail(CDA_ERR_INVALID, "eds capacity too small");
+        return e.host_construct_extend_dah(p, txs, n_txs ? tx_off[n_txs] : 0, eds, row_roots, col_roots, data_root);
+    });
+}
+
+int cda_square_construct_device(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs,
+                                const void* d_txs, uint32_t max_square_size, uint32_t threshold, int mode,
+                                void* d_ods, size_t ods_capacity, uint32_t* square_size, uint32_t* kept,
+                                uint32_t* n_kept, void* stream) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!d_ods || !square_size || (n_txs && (!txs || !tx_off || !d_txs)))
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda::square::Plan p;
+        std::string err;
+        if (plan_square(txs, tx_off, n_txs, max_square_size, threshold, mode, &p, &err))
+            return e.fail(CDA_ERR_SQUARE, err);
+        *square_size = p.square_size;
+        if (kept) {
+            memcpy(kept, p.kept.data(), p.kept.size() * 4);
+            if (n_kept) *n_kept = (uint32_t)p.kept.size();
+        }
+        if ((size_t)p.square_size * p.square_size * CDA_SHARE_SIZE > ods_capacity)
+            return e.fail(CDA_ERR_INVALID, "ods capacity too small for the square");
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
+        return e.enqueue_square(p, static_cast<const uint8_t*>(d_txs), static_cast<uint8_t*>(d_ods), s);
     });
 }
 

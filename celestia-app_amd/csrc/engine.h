@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "cda_kernels.h"
+#include "square_plan.h"
 
 namespace cda {
 
@@ -64,6 +65,15 @@ class Engine {
     int host_rs(const uint8_t* data, uint32_t k, uint32_t len, uint32_t n, uint8_t* parity);
     int host_data_root(const uint8_t* rows, const uint8_t* cols, uint32_t w, uint8_t* root);
 
+    // Square construction (square.hip): the layout is planned on the host
+    // (square_plan.cpp), the shares are written on the device.
+    // d_txs: the transaction bytes the plan's offsets refer to, with >= 16
+    // bytes of readable slack after the end.
+    int enqueue_square(const square::Plan& p, const uint8_t* d_txs, uint8_t* d_ods, hipStream_t s);
+    int host_square(const square::Plan& p, const uint8_t* txs, size_t txs_len, uint8_t* ods);
+    int host_construct_extend_dah(const square::Plan& p, const uint8_t* txs, size_t txs_len, uint8_t* eds,
+                                  uint8_t* rows, uint8_t* cols, uint8_t* root);
+
     // Stage timing with HIP events on the launch stream (bench / profiling).
     enum Stage { kStageRsQ0 = 0, kStageRsQ3, kStageOrder, kStageLeaves, kStageLevels, kStageDataRoot, kNumStages };
     void set_profiling(bool on) { profiling_ = on; }
@@ -110,6 +120,13 @@ class Engine {
     Gf16Dev gf16(uint32_t k) const;
     DevBuf leaf_, lvl_, root_slots_, dig_, err_buf_;
     DevBuf h_ods_, h_eds_, h_rows_, h_cols_, h_roots_;   // device staging for host-buffer calls
+    // square construction: device plan (segments + compact shares), device
+    // copy of host txs, pinned staging for the plan and its copy-done event
+    DevBuf sq_plan_, sq_txs_;
+    void* sq_stage_ = nullptr;
+    size_t sq_stage_bytes_ = 0;
+    hipEvent_t sq_event_ = nullptr;
+    int upload_txs(const uint8_t* txs, size_t len, hipStream_t s);
 };
 
 }  // namespace cda

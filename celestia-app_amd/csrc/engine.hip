@@ -47,8 +47,10 @@ Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
     for (DevBuf* b : {&gf16_chunk_[0], &gf16_chunk_[1], &gf16_log_, &gf16_exp_,
                       &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &h_ods_, &h_eds_,
-                      &h_rows_, &h_cols_, &h_roots_})
+                      &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_})
         b->release();
+    if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
+    if (sq_stage_) (void)hipHostFree(sq_stage_);
     for (Mark& m : marks_) {
         if (m.a) (void)hipEventDestroy(m.a);
         if (m.b) (void)hipEventDestroy(m.b);

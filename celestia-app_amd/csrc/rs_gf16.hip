@@ -37,7 +37,6 @@ namespace cda {
 namespace {
 
 constexpr uint32_t kMod16 = 65535;
-constexpr size_t SH = 512;
 
 // ---------------------------------------------------------------------------
 // register-resident codeword kernel

@@ -21,6 +21,11 @@
  *   cda_data_root          (*DataAvailabilityHeader).Hash
  *                          pkg/da/data_availability_header.go:92-108
  *   cda_extend_dah_device  device-resident batch (inputs/outputs in HBM)
+ *   cda_square_layout / cda_square_construct / cda_construct_extend_dah /
+ *   cda_square_construct_device
+ *                          go-square square.Construct / square.Build (EXT
+ *                          v1.1.0, go.mod:9; app/process_proposal.go:122,
+ *                          app/prepare_proposal.go:50, app/extend_block.go:16)
  *
  * Conventions
  *   - All buffers are plain byte arrays; shares are row-major and contiguous
@@ -59,7 +64,8 @@ enum {
     CDA_ERR_DEVICE = -4,        /* HIP runtime / kernel launch failure */
     CDA_ERR_OOM = -5,           /* device allocation failure */
     CDA_ERR_INVALID = -6,       /* bad argument (NULL pointer, k out of range, ...) */
-    CDA_ERR_UNSUPPORTED = -7    /* shard count the codec does not support */
+    CDA_ERR_UNSUPPORTED = -7,   /* shard count the codec does not support */
+    CDA_ERR_SQUARE = -8         /* go-square square.Construct / Build error (message from cda_last_error) */
 };
 
 typedef struct cda_ctx cda_ctx;
@@ -143,6 +149,56 @@ int cda_split_cols(cda_ctx *ctx, void *d_col_block, uint32_t k, uint32_t n_cols,
 int cda_split_combine(cda_ctx *ctx, const void *d_row_subtree_slots, uint32_t parts, uint32_t k,
                       const void *d_col_root_slots, void *d_row_roots, void *d_col_roots, void *d_data_root,
                       void *stream);
+
+/* ---- Data-square construction ----------------------
+ * go-square v1.1.0 square.Construct (mode CDA_SQUARE_CONSTRUCT; used by
+ * ProcessProposal app/process_proposal.go:122-126 and ExtendBlock
+ * app/extend_block.go:16-20) and square.Build (mode CDA_SQUARE_BUILD;
+ * PrepareProposal app/prepare_proposal.go:50-53).  Construct fails on a tx
+ * that does not fit or a normal tx after a blob tx; Build skips txs that do
+ * not fit and returns the kept ones.
+ *   txs, tx_off: the block's n_txs transactions concatenated; tx i is
+ *     txs[tx_off[i] .. tx_off[i+1]) (tx_off has n_txs + 1 entries).
+ *   max_square_size: appconsts.SquareSizeUpperBound / GovMaxSquareSize
+ *     (power of two); threshold: appconsts.SubtreeRootThreshold (64).
+ *   square_size: out, the ODS width k (dataSquare.Size()).
+ *   kept (n_txs entries, may be NULL) / n_kept: indexes of the txs in the
+ *     square in block order (normal txs, then blob txs) -- Build's txs result.
+ * Errors: CDA_ERR_SQUARE with go-square's message (cda_last_error). */
+#define CDA_SQUARE_CONSTRUCT 0
+#define CDA_SQUARE_BUILD 1
+
+/* Layout only, on the host (no device work; ctx may be NULL, then the error
+ * message is cda_last_error(NULL) of the calling thread).  share_indexes
+ * receives the start share of every blob, per PFB in square order and blob
+ * order within the PFB (the IndexWrapper.share_indexes written to the square). */
+int cda_square_layout(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, uint32_t n_txs,
+                      uint32_t max_square_size, uint32_t threshold, int mode, uint32_t *square_size, uint32_t *kept,
+                      uint32_t *n_kept, uint32_t *share_indexes, uint32_t share_index_cap, uint32_t *n_share_indexes);
+
+/* The square's k*k shares (row-major) into ods (host, ods_capacity bytes;
+ * max_square_size^2 * 512 always suffices).  Shares are written on the GPU. */
+int cda_square_construct(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, uint32_t n_txs,
+                         uint32_t max_square_size, uint32_t threshold, int mode, uint8_t *ods, size_t ods_capacity,
+                         uint32_t *square_size, uint32_t *kept, uint32_t *n_kept);
+
+/* Construct + ExtendShares + NewDataAvailabilityHeader in one submission (the
+ * proposal paths' whole DA step); the ODS never leaves HBM.  eds may be NULL;
+ * row_roots / col_roots hold roots_capacity bytes each (2 * max_square_size *
+ * 90 always suffices); data_root = 32 bytes. */
+int cda_construct_extend_dah(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, uint32_t n_txs,
+                             uint32_t max_square_size, uint32_t threshold, int mode, uint8_t *eds, size_t eds_capacity,
+                             uint8_t *row_roots, uint8_t *col_roots, size_t roots_capacity, uint8_t *data_root,
+                             uint32_t *square_size, uint32_t *kept, uint32_t *n_kept);
+
+/* Device variant: the layout is planned from the host txs, the shares are
+ * written from d_txs (a device copy of the same bytes with >= 16 readable
+ * bytes after the end) into d_ods; only enqueues on stream (NULL = HIP's
+ * default stream). */
+int cda_square_construct_device(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, uint32_t n_txs,
+                                const void *d_txs, uint32_t max_square_size, uint32_t threshold, int mode,
+                                void *d_ods, size_t ods_capacity, uint32_t *square_size, uint32_t *kept,
+                                uint32_t *n_kept, void *stream);
 
 /* Stage timing (HIP events on the launch stream).  When enabled, every
  * enqueued stage is bracketed by events; cda_stage_times synchronises them and

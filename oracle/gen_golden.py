@@ -5,10 +5,14 @@ TEST INFRASTRUCTURE.  Run in the container that has /root/reference:
 Outputs (committed; the GPU box never reads /root/reference):
   tests/golden/block408_ods.bin.gz  -- ODS of mainnet block 408 (k=32) built by
       oracle/square.py from x/blob/test/testdata/block_response.json
+  tests/golden/block408_txs.json.gz -- the block's txs (base64), square size
+      and header.data_hash, copied from that reference fixture (data only) so
+      GPU tests can run square construction without /root/reference
   tests/golden/golden.json          -- expected data roots: the reference's
       golden hashes (pkg/da/data_availability_header_test.go) and the block's
       data_hash, plus oracle digests of random squares (seeded SplitMix64).
 """
+import base64
 import gzip
 import hashlib
 import json
@@ -41,6 +45,9 @@ def main():
         "constant_k128": "0bd3abeeacfbb0b92dfbdac4a154868e3c4e79666f7fcf6c620bb90dd3a0dcf0",
     }}
     txs, k, data_hash = square.load_block(os.path.join(REF, "x/blob/test/testdata/block_response.json"))
+    with gzip.open(os.path.join(OUT, "block408_txs.json.gz"), "wt", compresslevel=9) as f:
+        json.dump({"height": 408, "square_size": k, "data_hash": data_hash.hex(),
+                   "txs": [base64.b64encode(t).decode() for t in txs]}, f)
     ods = np.frombuffer(b"".join(square.construct(txs, k)), dtype=np.uint8).reshape(k * k, 512)
     with gzip.open(os.path.join(OUT, "block408_ods.bin.gz"), "wb", compresslevel=9) as f:
         f.write(ods.tobytes())

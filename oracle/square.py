@@ -105,7 +105,8 @@ def unmarshal_blob_tx(tx: bytes):
 def marshal_index_wrapper(tx: bytes, share_indexes) -> bytes:
     """IndexWrapper{tx=1, share_indexes=2 (packed), type_id=3 = "INDX"} (gogoproto order)."""
     out = bytearray()
-    out += b"\x0a" + _enc_varint(len(tx)) + tx
+    if tx:
+        out += b"\x0a" + _enc_varint(len(tx)) + tx
     if share_indexes:
         packed = b"".join(_enc_varint(x) for x in share_indexes)
         out += b"\x12" + _enc_varint(len(packed)) + packed
@@ -221,8 +222,15 @@ class CompactShareCounter:
     def __init__(self):
         self.shares = 0
         self.remainder = 0
+        self.last = (0, 0)
 
-    def add(self, data_len: int):
+    def revert(self):
+        self.shares, self.remainder = self.last
+
+    def add(self, data_len: int) -> int:
+        """Returns the change of size() (the Go counter's diff)."""
+        before = self.size()
+        self.last = (self.shares, self.remainder)
         data_len += len(_enc_varint(data_len))
         if self.shares == 0:
             if data_len >= FIRST_COMPACT_CONTENT - self.remainder:
@@ -242,6 +250,7 @@ class CompactShareCounter:
         if data_len > 0:
             self.shares += data_len // CONT_COMPACT_CONTENT
             self.remainder = data_len % CONT_COMPACT_CONTENT
+        return self.size() - before
 
     def size(self) -> int:
         return self.shares if self.remainder == 0 else self.shares + 1
@@ -303,3 +312,102 @@ def load_block(path: str):
     k = int(d["data"]["square_size"])
     data_hash = base64.b64decode(d["header"]["data_hash"])
     return txs, k, data_hash
+
+
+# ------------------------------------------------- builder (Construct / Build)
+def _valid_blob_namespace(ns_version: int, ns_id: bytes) -> bool:
+    """namespace.New checks run by SparseShareSplitter.Write."""
+    if ns_version not in (0, 255) or len(ns_id) != NS_SIZE - 1:
+        return False
+    return ns_version != 0 or ns_id[:18] == b"\x00" * 18
+
+
+def builder(txs, max_square_size: int = 128, threshold: int = SUBTREE_ROOT_THRESHOLD, mode: str = "construct"):
+    """go-square square.Construct (mode "construct") / square.Build ("build"):
+    NewBuilder + AppendTx / AppendBlobTx (worst-case share accounting, canFit
+    against max_square_size^2) + Export (square size = BlobMinSquareSize of the
+    worst-case total) + WriteSquare.  Structure as in the reference's copy,
+    test/util/malicious/out_of_order_builder.go:24-161.
+
+    Returns (shares, square_size, kept tx indexes, share indexes per blob in
+    PFB order); raises ValueError with go-square's message."""
+    cap = max_square_size * max_square_size
+    txc, pfbc = CompactShareCounter(), CompactShareCounter()
+    current = 0
+    normal, normal_idx, blob_idx, pfbs, elems = [], [], [], [], []
+    seen_blob = False
+    for t, tx in enumerate(txs):
+        bt = unmarshal_blob_tx(tx)
+        if bt is not None:
+            seen_blob = True
+            inner, bl = bt
+            diff = pfbc.add(len(marshal_index_wrapper(inner, [WORST_CASE_SHARE_INDEX] * len(bl))))
+            es, worst = [], 0
+            for bi, b in enumerate(bl):
+                n = sparse_share_count(len(b["data"])) if b["data"] else 0
+                maxpad = subtree_width(n, threshold) - 1
+                worst += n + maxpad
+                ns_version = b["namespace_version"] & 0xFF
+                es.append(dict(ns=bytes([ns_version]) + b["namespace_id"], ns_version=ns_version,
+                               ns_id=b["namespace_id"], data=b["data"], ver=b["share_version"],
+                               pfb=len(pfbs), bi=bi, n=n, maxpad=maxpad))
+            if current + diff + worst <= cap:
+                current += diff + worst
+                elems += es
+                pfbs.append([inner, [0] * len(bl)])
+                blob_idx.append(t)
+            else:
+                pfbc.revert()
+                if mode == "construct":
+                    raise ValueError(f"not enough space to append blob tx at index {t}")
+        else:
+            if mode == "construct" and seen_blob:
+                raise ValueError(f"normal transaction at index {t} can not be appended after blob tx")
+            diff = txc.add(len(tx))
+            if current + diff <= cap:
+                current += diff
+                normal.append(tx)
+                normal_idx.append(t)
+            else:
+                txc.revert()
+                if mode == "construct":
+                    raise ValueError(f"not enough space to append tx at index {t}")
+    kept = normal_idx + blob_idx
+    if not normal and not pfbs:
+        return [padding_share(TAIL_PADDING_NS)], 1, kept, []
+    ss = blob_min_square_size(current)
+    elems.sort(key=lambda e: e["ns"])                       # stable
+    tx_shares = compact_shares(TX_NS, normal)
+    cursor = end_of_last = non_reserved_start = txc.size() + pfbc.size()
+    blob_part = []
+    for i, e in enumerate(elems):
+        cursor = next_share_index(cursor, e["n"], threshold)
+        if i == 0:
+            non_reserved_start = cursor
+        padding = cursor - end_of_last
+        if padding > e["maxpad"]:
+            raise ValueError(f"blob has {padding} padding shares, but {e['maxpad']} was the max possible")
+        pfbs[e["pfb"]][1][e["bi"]] = cursor
+        if i > 0 and padding:
+            if not blob_part:
+                raise ValueError("cannot write namespace padding shares on an empty SparseShareSplitter")
+            blob_part += [padding_share(blob_part[-1][:NS_SIZE])] * padding
+        if e["ver"] & 0xFF != 0:
+            raise ValueError(f"unsupported share version: {e['ver'] & 0xFF}")
+        if not _valid_blob_namespace(e["ns_version"], e["ns_id"]):
+            raise ValueError("invalid blob namespace")
+        if e["n"]:
+            blob_part += sparse_shares(e["ns"], e["data"], 0)
+        cursor += e["n"]
+        end_of_last = cursor
+    pfb_shares = compact_shares(PFB_NS, [marshal_index_wrapper(t, idx) for t, idx in pfbs])
+    total = ss * ss
+    if non_reserved_start < len(tx_shares) + len(pfb_shares):
+        raise ValueError("nonReservedStart is too small to fit all PFBs and txs")
+    square = list(tx_shares) + list(pfb_shares)
+    square += [padding_share(PRIMARY_RESERVED_PADDING_NS)] * (non_reserved_start - len(square))
+    square += blob_part
+    if len(square) > total:
+        raise ValueError(f"square size {total} is too small to fit all blobs")
+    square += [padding_share(TAIL_PADDING_NS)] * (total - len(square))
+    return square, ss, kept, [i for _, idx in pfbs for i in idx]

@@ -1,0 +1,188 @@
+"""Data-square construction (go-square square.Construct / Build), SURVEY.md
+8(f) row 1.
+
+Pins:
+  * mainnet block 408 (tests/golden/block408_txs.json.gz, copied from the
+    reference fixture x/blob/test/testdata/block_response.json): the square
+    size computed from the txs equals the block's square_size, the ODS equals
+    the one whose data root is header.data_hash, and the whole txs -> data
+    root path reproduces header.data_hash;
+  * synthetic blocks (celestia_da.blobfactory, seeded) against the oracle's
+    Builder restatement (oracle/square.py `builder`).
+CPU tests exercise the host layout planner (no device work); `gpu` tests the
+share writer and the fused construct + extend + DAH path.
+"""
+import base64
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+import coracle
+import square as osq
+from celestia_da import SquareError, blobfactory
+from celestia_da import square as gsq
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def block408():
+    with gzip.open(os.path.join(HERE, "golden", "block408_txs.json.gz"), "rt") as f:
+        d = json.load(f)
+    return [base64.b64decode(t) for t in d["txs"]], d["square_size"], bytes.fromhex(d["data_hash"])
+
+
+def block408_ods():
+    with gzip.open(os.path.join(HERE, "golden", "block408_ods.bin.gz")) as f:
+        return f.read()
+
+
+CASES = [
+    # (seed, n_normal, n_blob_txs, blobs_per_tx, blob_size, shared_ns, max_square_size)
+    (1, 4, 10, (1, 2), (1, 3000), 0, 32),
+    (2, 0, 40, (1, 4), (1, 40000), 0, 64),
+    (3, 12, 25, (1, 3), (400, 30000), 3, 64),
+    (4, 6, 120, (1, 3), (1, 60000), 0, 128),
+    (5, 30, 0, (1, 1), (1, 1), 0, 16),          # normal txs only
+    (6, 0, 3, (1, 1), (477, 479), 0, 8),        # first-share boundary sizes
+    (7, 2, 60, (2, 5), (1, 900), 5, 128),       # many small blobs, shared namespaces
+]
+
+
+def case_txs(c):
+    seed, nn, nb, bpt, bs, shared, _ = c
+    return blobfactory.random_block(seed, nn, nb, bpt, bs, shared)
+
+
+# ------------------------------------------------------------------ CPU tests
+def test_block408_layout():
+    txs, k, _ = block408()
+    ss, kept, idx = gsq.layout(txs)
+    o_sh, o_ss, o_kept, o_idx = osq.builder(txs)
+    assert ss == o_ss == k == 32
+    assert kept == o_kept == list(range(len(txs)))
+    assert idx == o_idx
+    assert b"".join(o_sh) == block408_ods()
+
+
+@pytest.mark.parametrize("c", CASES, ids=[f"seed{c[0]}" for c in CASES])
+@pytest.mark.parametrize("mode", ["construct", "build"])
+def test_layout_matches_oracle(c, mode):
+    txs = case_txs(c)
+    max_ss = c[-1]
+    try:
+        want = osq.builder(txs, max_ss, 64, mode)
+    except ValueError as e:
+        with pytest.raises(SquareError):
+            gsq.layout(txs, max_ss, 64, build=mode == "build")
+        assert mode == "construct", e
+        return
+    ss, kept, idx = gsq.layout(txs, max_ss, 64, build=mode == "build")
+    assert (ss, kept, idx) == (want[1], want[2], want[3])
+
+
+def test_build_drops_what_does_not_fit():
+    txs = blobfactory.random_block(11, 2, 80, (1, 2), (20000, 60000))
+    ss, kept, _ = gsq.layout(txs, 32, 64, build=True)
+    assert ss <= 32 and 0 < len(kept) < len(txs)
+    with pytest.raises(SquareError, match="not enough space to append blob tx"):
+        gsq.layout(txs, 32, 64)
+
+
+def test_normal_tx_after_blob_tx():
+    rng = np.random.default_rng(3)
+    txs = blobfactory.random_block(12, 1, 2) + [blobfactory.normal_tx(rng, 100)]
+    with pytest.raises(SquareError, match="normal transaction at index 3 can not be appended after blob tx"):
+        gsq.layout(txs)
+    ss, kept, _ = gsq.layout(txs, build=True)      # Build reorders: normal txs first
+    assert kept == [0, 3, 1, 2]
+
+
+def test_empty_block_is_min_square():
+    assert gsq.layout([]) == (1, [], [])
+    sh, ss, _, _ = osq.builder([])
+    assert ss == 1 and sh == [osq.padding_share(osq.TAIL_PADDING_NS)]
+
+
+def test_invalid_blob_namespace_rejected():
+    bad = blobfactory.blob_tx(b"x" * 50, [(b"\x01" * 28, b"data")])      # version 0 without the 18 zero bytes
+    with pytest.raises(SquareError, match="namespace"):
+        gsq.layout([bad])
+    with pytest.raises(ValueError):
+        osq.builder([bad])
+
+
+def test_unsupported_share_version_rejected():
+    ns = b"\x00" * 18 + b"\x07" * 10
+    bad = blobfactory.blob_tx(b"x" * 50, [(ns, b"data", 1)])
+    with pytest.raises(SquareError, match="unsupported share version"):
+        gsq.layout([bad])
+
+
+def test_not_a_blob_tx_is_normal():
+    # wrong type_id, truncated protobuf, empty tx: all plain txs
+    ns = b"\x00" * 18 + b"\x07" * 10
+    good = blobfactory.blob_tx(b"x" * 50, [(ns, b"data")])
+    txs = [good.replace(b"BLOB", b"BLOC"), good[:-3], b""]
+    ss, kept, idx = gsq.layout(txs)
+    assert kept == [0, 1, 2] and idx == []
+    assert osq.builder(txs)[2] == kept
+
+
+# ------------------------------------------------------------------ GPU tests
+@pytest.mark.gpu
+def test_block408_construct_gpu(ctx):
+    txs, k, data_hash = block408()
+    sq = gsq.construct(txs)
+    assert sq.size() == k and sq.to_bytes() == block408_ods()
+    kk, _, rows, cols, root, kept = gsq.construct_extend_dah(txs)
+    assert kk == k and root == data_hash and kept == list(range(len(txs)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", CASES, ids=[f"seed{c[0]}" for c in CASES])
+def test_construct_gpu_matches_oracle(ctx, c):
+    txs = case_txs(c)
+    max_ss = c[-1]
+    sh, ss, kept, _ = osq.builder(txs, max_ss, 64, "build")
+    sq, kept_txs = gsq.build(txs, max_ss, 64)
+    assert sq.size() == ss
+    assert sq.to_bytes() == b"".join(sh)
+    assert kept_txs == [txs[i] for i in kept]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", CASES[:4], ids=[f"seed{c[0]}" for c in CASES[:4]])
+def test_construct_extend_dah_gpu(ctx, c):
+    txs = case_txs(c)
+    max_ss = c[-1]
+    sh, ss, _, _ = osq.builder(txs, max_ss, 64, "build")
+    ods = np.frombuffer(b"".join(sh), dtype=np.uint8).reshape(-1, 512).copy()
+    e_eds, e_rows, e_cols, e_root = coracle.cpu_baseline(ods, 8) if ss >= 64 else coracle.extend_dah(ods)
+    k, eds, rows, cols, root, _ = gsq.construct_extend_dah(txs, max_ss, 64, build_mode=True, want_eds=True)
+    assert k == ss
+    assert eds == e_eds.tobytes()
+    assert rows == [bytes(r) for r in e_rows] and cols == [bytes(x) for x in e_cols]
+    assert root == e_root
+
+
+@pytest.mark.gpu
+def test_construct_device_variant(ctx):
+    import ctypes as C
+
+    import torch
+    txs = case_txs(CASES[3])
+    sh, ss, _, _ = osq.builder(txs, 128, 64, "build")
+    buf, off = gsq._flatten(txs)
+    d_txs = torch.zeros(buf.size + 16, dtype=torch.uint8, device="cuda")
+    d_txs[:buf.size] = torch.from_numpy(buf).cuda()
+    d_ods = torch.empty(128 * 128 * 512, dtype=torch.uint8, device="cuda")
+    k = C.c_uint32()
+    ctx.check(ctx.lib.cda_square_construct_device(ctx.h, gsq.ptr(buf), gsq._u64p(off), len(txs), d_txs.data_ptr(),
+                                                  128, 64, 1, d_ods.data_ptr(), d_ods.numel(), C.byref(k), None, None,
+                                                  None))
+    torch.cuda.synchronize()
+    assert k.value == ss
+    assert d_ods[:ss * ss * 512].cpu().numpy().tobytes() == b"".join(sh)
