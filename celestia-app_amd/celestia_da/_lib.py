@@ -40,6 +40,7 @@ EXPORTED = (
     "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
+    "cda_blob_commitments", "cda_blob_commitments_device",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -109,6 +110,8 @@ def load():
                                                C.c_size_t, u8p, u8p, C.c_size_t, u8p, u32p, u32p, u32p]
         L.cda_square_construct_device.argtypes = [ctxp, u8p, u64p, C.c_uint32, vp, C.c_uint32, C.c_uint32, C.c_int,
                                                   vp, C.c_size_t, u32p, u32p, u32p, vp]
+        L.cda_blob_commitments.argtypes = [ctxp, u8p, u8p, u64p, u8p, C.c_uint32, C.c_uint32, u8p]
+        L.cda_blob_commitments_device.argtypes = [ctxp, u8p, u64p, u8p, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L

@@ -323,6 +323,37 @@ int cda_square_construct_device(cda_ctx* ctx, const uint8_t* txs, const uint64_t
     });
 }
 
+int cda_blob_commitments(cda_ctx* ctx, const uint8_t* namespaces, const uint8_t* data, const uint64_t* data_off,
+                         const uint8_t* share_versions, uint32_t n, uint32_t threshold, uint8_t* commitments) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (n == 0) return CDA_OK;
+        if (!namespaces || !data_off || !commitments || (data_off[n] > data_off[0] && !data))
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda::square::CommitPlan p;
+        std::string err;
+        if (cda::square::plan_commitments(namespaces, data_off, share_versions, n, threshold, &p, &err))
+            return e.fail(CDA_ERR_SQUARE, err);
+        return e.host_commitments(p, n, data, (size_t)data_off[n], commitments);
+    });
+}
+
+int cda_blob_commitments_device(cda_ctx* ctx, const uint8_t* namespaces, const uint64_t* data_off,
+                                const uint8_t* share_versions, uint32_t n, uint32_t threshold, const void* d_data,
+                                void* d_commitments, void* stream) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (n == 0) return CDA_OK;
+        if (!namespaces || !data_off || !d_commitments || (data_off[n] > data_off[0] && !d_data))
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda::square::CommitPlan p;
+        std::string err;
+        if (cda::square::plan_commitments(namespaces, data_off, share_versions, n, threshold, &p, &err))
+            return e.fail(CDA_ERR_SQUARE, err);
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
+        return e.enqueue_commitments(p, n, static_cast<const uint8_t*>(d_data), static_cast<uint8_t*>(d_commitments),
+                                     s);
+    });
+}
+
 int cda_set_profiling(cda_ctx* ctx, int enable) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
         e.set_profiling(enable != 0);

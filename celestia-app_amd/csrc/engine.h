@@ -14,6 +14,10 @@
 
 namespace cda {
 
+// square.hip: writes n_shares shares of a square::Plan / CommitPlan layout.
+hipError_t launch_share_writer(const square::Segment* segs, uint32_t n_segs, const uint8_t* compact,
+                               const uint8_t* txs, uint8_t* ods, uint32_t n_shares, hipStream_t s);
+
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
@@ -74,6 +78,13 @@ class Engine {
     int host_construct_extend_dah(const square::Plan& p, const uint8_t* txs, size_t txs_len, uint8_t* eds,
                                   uint8_t* rows, uint8_t* cols, uint8_t* root);
 
+    // Blob share commitments (commit.hip).  d_data: blob bytes the plan's
+    // offsets refer to (>= 16 readable bytes of slack); d_out: n_blobs * 32.
+    int enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* d_data, uint8_t* d_out,
+                            hipStream_t s);
+    int host_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* data, size_t data_len,
+                         uint8_t* out);
+
     // Stage timing with HIP events on the launch stream (bench / profiling).
     enum Stage { kStageRsQ0 = 0, kStageRsQ3, kStageOrder, kStageLeaves, kStageLevels, kStageDataRoot, kNumStages };
     void set_profiling(bool on) { profiling_ = on; }
@@ -123,6 +134,7 @@ class Engine {
     // square construction: device plan (segments + compact shares), device
     // copy of host txs, pinned staging for the plan and its copy-done event
     DevBuf sq_plan_, sq_txs_;
+    DevBuf cm_plan_, cm_shares_, cm_leaf_, cm_lvl_, cm_roots_, cm_out_;   // commitments
     void* sq_stage_ = nullptr;
     size_t sq_stage_bytes_ = 0;
     hipEvent_t sq_event_ = nullptr;

@@ -51,20 +51,6 @@ __device__ __forceinline__ void bswap16(uint32_t (&w)[16]) {
 #pragma unroll
     for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);
 }
-__device__ __forceinline__ void load_slot_be(const uint8_t* slot, uint32_t (&w)[kSlotWords]) {
-    const uint4* p = reinterpret_cast<const uint4*>(slot);
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        const uint4 v = p[q];
-        w[4 * q + 0] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y);
-        w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
-    }
-}
-__device__ __forceinline__ void store_slot(uint8_t* slot, const uint32_t (&w)[kSlotWords]) {
-    uint4* p = reinterpret_cast<uint4*>(slot);
-#pragma unroll
-    for (int q = 0; q < 6; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-}
 
 // ---------------------------------------------------------------------------
 // Q0 push-order check (nmt ErrInvalidPushOrder on any row or column of Q0).

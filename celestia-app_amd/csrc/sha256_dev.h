@@ -169,6 +169,22 @@ CDA_HD void inner_node_words(const uint32_t* L, const uint32_t* R, const uint32_
     for (int t = 0; t < kSlotWords; t++) out[t] = bswap32(be[t]);
 }
 
+// 96-B node slots: big-endian word view on load, little-endian words on store.
+CDA_HD void load_slot_be(const uint8_t* slot, uint32_t (&w)[kSlotWords]) {
+    const uint4* p = reinterpret_cast<const uint4*>(slot);
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        const uint4 v = p[q];
+        w[4 * q + 0] = bswap32(v.x); w[4 * q + 1] = bswap32(v.y);
+        w[4 * q + 2] = bswap32(v.z); w[4 * q + 3] = bswap32(v.w);
+    }
+}
+CDA_HD void store_slot(uint8_t* slot, const uint32_t (&w)[kSlotWords]) {
+    uint4* p = reinterpret_cast<uint4*>(slot);
+#pragma unroll
+    for (int q = 0; q < 6; q++) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
 // ---------------------------------------------------------------------------
 // RFC-6962 (go-square/merkle): leaf = sha256(0x00 || item90), inner =
 // sha256(0x01 || a32 || b32).  I = big-endian words of a 96-B slot.

@@ -583,5 +583,94 @@ int plan(const uint8_t* txs, const uint64_t* off, uint32_t n, uint32_t max_ss, u
     return 0;
 }
 
+// inclusion.CreateCommitment layout for a batch of blobs: SplitBlobs (sparse
+// shares), SubTreeWidth, MerkleMountainRangeSizes.  Validation follows
+// SparseShareSplitter.Write (share version, namespace.New).
+int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const uint8_t* share_versions, uint32_t n,
+                     uint32_t threshold, CommitPlan* out, std::string* err) {
+    CommitPlan& P = *out;
+    P = CommitPlan{};
+    if (threshold == 0) {
+        *err = "subtree root threshold must be positive";
+        return -1;
+    }
+    P.blob_tree0.reserve(n + 1);
+    uint64_t cursor = 0;
+    for (uint32_t b = 0; b < n; b++) {
+        P.blob_tree0.push_back((uint32_t)P.trees.size());
+        const uint8_t* ns = namespaces + (size_t)b * kNs;
+        const uint8_t ver = share_versions ? share_versions[b] : 0;
+        if (ver != 0) {
+            *err = fmt("blob %lld: unsupported share version: %lld", b, ver);
+            return -1;
+        }
+        if (ns[0] != 0 && ns[0] != 255) {
+            *err = fmt("blob %lld: unsupported namespace version %lld", b, ns[0]);
+            return -1;
+        }
+        if (ns[0] == 0)
+            for (int z = 1; z < 19; z++)
+                if (ns[z]) {
+                    *err = fmt("blob %lld: unsupported namespace id with version 0: ID must start with 18 leading "
+                               "zeros",
+                               b);
+                    return -1;
+                }
+        if (data_off[b + 1] < data_off[b]) {
+            *err = "blob offsets must be non-decreasing";
+            return -1;
+        }
+        const uint64_t len = data_off[b + 1] - data_off[b];
+        if (len > 0xFFFFFFFFull) {
+            *err = "blob too large";
+            return -1;
+        }
+        const uint32_t n_sh = sparse_shares_needed((uint32_t)len);
+        if (n_sh == 0) continue;   // nil data: no shares, commitment = sha256("")
+        const uint32_t w = subtree_width(n_sh, threshold);
+        const uint64_t start = (cursor + w - 1) / w * w;
+        if (start > cursor) {   // alignment gap (never hashed into a used node)
+            Segment g{};
+            g.kind = kSegPadding;
+            g.start = (uint32_t)cursor;
+            g.n = (uint32_t)(start - cursor);
+            P.segs.push_back(g);
+        }
+        Segment s{};
+        s.kind = kSegBlob;
+        s.start = (uint32_t)start;
+        s.n = n_sh;
+        s.version = ver;
+        s.src = data_off[b];
+        s.len = (uint32_t)len;
+        std::memcpy(s.ns, ns, kNs);
+        P.segs.push_back(s);
+        uint32_t left = n_sh, off = (uint32_t)start, nt = 0;
+        while (left) {   // inclusion.MerkleMountainRangeSizes
+            uint32_t size = w;
+            if (left < w) {
+                size = 1;
+                while (size * 2 <= left) size *= 2;
+            }
+            uint32_t h = 0;
+            while ((1u << h) < size) h++;
+            P.trees.push_back(Tree{off, h});
+            P.max_height = std::max(P.max_height, h);
+            off += size;
+            left -= size;
+            nt++;
+        }
+        P.max_trees = std::max(P.max_trees, nt);
+        cursor = start + n_sh;
+        if (cursor > 0x7FFFFFFFull) {
+            *err = "blob batch too large";
+            return -1;
+        }
+    }
+    P.blob_tree0.push_back((uint32_t)P.trees.size());
+    P.n_leaves = (uint32_t)cursor;
+    return 0;
+}
+
 }  // namespace square
 }  // namespace cda

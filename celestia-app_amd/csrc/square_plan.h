@@ -63,6 +63,28 @@ enum Mode { kConstruct = 0, kBuild = 1 };
 int plan(const uint8_t* txs, const uint64_t* off, uint32_t n, uint32_t max_square_size, uint32_t threshold, Mode mode,
          Plan* out, std::string* err);
 
+// ---- blob share commitments (go-square v1.1.0 inclusion.CreateCommitment) ----
+// Every blob's sparse shares are laid out in one leaf array, each blob starting
+// at a multiple of its subtree width w, so every Merkle-mountain-range subtree
+// (sizes w, ..., then decreasing powers of two) is a perfect tree aligned to
+// its size: level L of all subtrees of all blobs is then one pairwise pass.
+struct Tree {
+    uint32_t off;      // first leaf (multiple of 1 << height)
+    uint32_t height;   // log2(size)
+};
+struct CommitPlan {
+    uint32_t n_leaves = 0;             // leaf array length (blobs + alignment gaps)
+    uint32_t max_height = 0;
+    uint32_t max_trees = 0;            // most subtree roots of one blob
+    std::vector<Segment> segs;         // share layout of the leaf array (blob segments + gaps)
+    std::vector<Tree> trees;           // all subtrees, blob order then MMR order
+    std::vector<uint32_t> blob_tree0;  // first tree of blob i (n + 1 entries: prefix sums)
+};
+// namespaces: n * 29 bytes; data_off: n + 1 offsets into the blob data;
+// share_versions: n bytes or NULL (all 0).
+int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const uint8_t* share_versions, uint32_t n,
+                     uint32_t threshold, CommitPlan* out, std::string* err);
+
 // Helpers shared with tests and other components (go-square inclusion / shares).
 uint32_t round_up_pow2(uint32_t x);
 uint32_t blob_min_square_size(uint32_t share_count);

@@ -200,6 +200,27 @@ int cda_square_construct_device(cda_ctx *ctx, const uint8_t *txs, const uint64_t
                                 void *d_ods, size_t ods_capacity, uint32_t *square_size, uint32_t *kept,
                                 uint32_t *n_kept, void *stream);
 
+/* ---- Blob share commitments --------------------------
+ * go-square v1.1.0 inclusion.CreateCommitment(blob, merkle.HashFromByteSlices,
+ * threshold) for n blobs at once (x/blob/types/blob_tx.go:98 ValidateBlobTx;
+ * x/blob/types/payforblob.go:53 CreateCommitments).
+ *   namespaces: n * 29 bytes (version || id); blob i's data is
+ *     data[data_off[i] .. data_off[i+1]) (data_off has n + 1 entries);
+ *   share_versions: n bytes or NULL (all ShareVersionZero);
+ *   threshold: appconsts.SubtreeRootThreshold (64);
+ *   commitments: n * 32 bytes.
+ * A blob with empty data commits to sha256("") (no shares).  Invalid share
+ * versions / namespaces: CDA_ERR_SQUARE with go-square's message. */
+int cda_blob_commitments(cda_ctx *ctx, const uint8_t *namespaces, const uint8_t *data, const uint64_t *data_off,
+                         const uint8_t *share_versions, uint32_t n, uint32_t threshold, uint8_t *commitments);
+/* Device variant: d_data is a device copy of the blob bytes with >= 16
+ * readable bytes after the end, d_commitments is device memory; namespaces /
+ * offsets / versions stay on the host (the layout is planned there).  Only
+ * enqueues on stream (NULL = HIP's default stream). */
+int cda_blob_commitments_device(cda_ctx *ctx, const uint8_t *namespaces, const uint64_t *data_off,
+                                const uint8_t *share_versions, uint32_t n, uint32_t threshold, const void *d_data,
+                                void *d_commitments, void *stream);
+
 /* Stage timing (HIP events on the launch stream).  When enabled, every
  * enqueued stage is bracketed by events; cda_stage_times synchronises them and
  * returns, per stage, the summed milliseconds and launch counts since the
