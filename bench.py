@@ -222,6 +222,72 @@ def square_construction(ctx, dev, stream, max_ss: int = 128, reps: int = 20) -> 
             "data_root": d_root.cpu().numpy().tobytes().hex()}
 
 
+def blob_commitments(ctx, dev, stream, n_blocks: int = 64, reps: int = 10) -> dict:
+    """inclusion.CreateCommitment for every blob of
+    n_blocks full k=128 blocks (blobfactory.full_block_blobs), blob bytes
+    resident in HBM (cda_blob_commitments_device); plus one block's blobs
+    (ProcessProposal's ValidateBlobTx sweep) as a latency figure.  Roofline:
+    SHA-256 issue slots (9 compressions per share, 3 per NMT inner node, 2 per
+    RFC-6962 node)."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from celestia_da import blobfactory
+    from celestia_da import inclusion as ginc
+
+    def setup(blocks):
+        ns, datas = [], []
+        for b in blocks:
+            for ns_id, data in blobfactory.full_block_blobs(100 + b, 128):
+                ns.append(b"\x00" + ns_id)
+                datas.append(data)
+        n = len(datas)
+        nsb = np.frombuffer(b"".join(ns), dtype=np.uint8).copy()
+        off = np.zeros(n + 1, dtype=np.uint64)
+        for i, d in enumerate(datas):
+            off[i + 1] = off[i] + len(d)
+        flat = np.frombuffer(b"".join(datas), dtype=np.uint8)
+        d_data = torch.zeros(flat.size + 16, dtype=torch.uint8, device=dev)
+        d_data[:flat.size] = torch.from_numpy(flat.copy()).to(dev)
+        d_out = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+        comp = sum(ginc.sha256_compressions(len(d)) for d in datas)
+        return n, nsb, off, d_data, d_out, comp
+
+    def measure(n, nsb, off, d_data, d_out):
+        offp = off.ctypes.data_as(C.POINTER(C.c_uint64))
+        nsp = nsb.ctypes.data_as(C.POINTER(C.c_uint8))
+
+        def run():
+            ctx.check(ctx.lib.cda_blob_commitments_device(ctx.h, nsp, offp, None, n, 64, d_data.data_ptr(),
+                                                          d_out.data_ptr(), stream))
+        run()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        wall = []
+        for e0, e1 in ev:
+            a = time.perf_counter()
+            e0.record()
+            run()
+            e1.record()
+            torch.cuda.synchronize(dev)
+            wall.append(time.perf_counter() - a)
+        return sorted(e0.elapsed_time(e1) for e0, e1 in ev)[reps // 2], 1e3 * sorted(wall)[reps // 2]
+
+    n, nsb, off, d_data, d_out, comp = setup(range(n_blocks))
+    ms, _ = measure(n, nsb, off, d_data, d_out)
+    slots = comp * SHA_SLOTS / (ms * 1e-3) / 1e12
+    n1, nsb1, off1, d1, o1, _ = setup([0])
+    ms1, wall1 = measure(n1, nsb1, off1, d1, o1)
+    return {"blobs": n, "blob_bytes": int(off[-1]), "ms": ms, "commitments_per_s": n / (ms * 1e-3),
+            "blob_gb_per_s": int(off[-1]) / (ms * 1e-3) / 1e9,
+            "roofline": {"bound": "valu", "achieved": slots, "peak": PEAK_VALU_TOPS, "unit": "T issue-slots/s",
+                         "frac": slots / PEAK_VALU_TOPS, "compressions": comp},
+            "one_block": {"blobs": n1, "blob_bytes": int(off1[-1]), "ms_device": ms1, "ms_wall": wall1},
+            "workload": f"all blobs of {n_blocks} full k=128 blocks (CheckTx/ProcessProposal ValidateBlobTx)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -326,6 +392,10 @@ def main():
             extras["square_construction"] = square_construction(ctx, dev, stream)
         except Exception as e:  # report, never lose the headline line
             extras["square_construction"] = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            extras["blob_commitments"] = blob_commitments(ctx, dev, stream)
+        except Exception as e:
+            extras["blob_commitments"] = {"error": f"{type(e).__name__}: {e}"}
         # config 3: one 512 x 512 square (GF(2^16), 512 MiB EDS)
         del d_eds
         torch.cuda.empty_cache()

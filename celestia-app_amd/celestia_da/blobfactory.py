@@ -80,19 +80,27 @@ def random_block(seed: int, n_normal: int = 8, n_blob_txs: int = 32, blobs_per_t
     return txs
 
 
-def full_block(seed: int, max_square_size: int = 128, fill: float = 0.95, blob_size=(2000, 200000)):
-    """Blob txs until about `fill` of max_square_size^2 shares are used (worst
-    case accounting), the config-2/4-sized workload for the construction bench."""
+def full_block_blobs(seed: int, max_square_size: int = 128, fill: float = 0.95, blob_size=(2000, 200000)):
+    """(namespace_id, data) pairs filling about `fill` of max_square_size^2
+    shares under the builder's worst-case accounting (shares + max padding,
+    priced here as 2x shares + 1 PFB share)."""
     rng = np.random.default_rng(seed)
     budget = int(fill * max_square_size * max_square_size)
-    txs, used = [], 0
+    out, used = [], 0
     while used < budget:
         size = int(rng.integers(blob_size[0], blob_size[1] + 1))
         shares = 1 + max(0, -(-(size - 478) // 482))
         if used + 2 * shares > budget:
             size = max(1, (budget - used) // 2 * 482)
             shares = 1 + max(0, -(-(size - 478) // 482))
-        inner = rng.integers(0, 256, 300, dtype=np.uint8).tobytes()
-        txs.append(blob_tx(inner, [(random_blob_namespace_id(rng), rng.integers(0, 256, size, dtype=np.uint8).tobytes())]))
+        out.append((random_blob_namespace_id(rng), rng.integers(0, 256, size, dtype=np.uint8).tobytes()))
         used += 2 * shares + 1
-    return txs
+    return out
+
+
+def full_block(seed: int, max_square_size: int = 128, fill: float = 0.95, blob_size=(2000, 200000)):
+    """One single-blob BlobTx per blob of full_block_blobs: the config-2/4-sized
+    workload for the construction bench."""
+    rng = np.random.default_rng(seed ^ 0x5EED)
+    return [blob_tx(rng.integers(0, 256, 300, dtype=np.uint8).tobytes(), [b])
+            for b in full_block_blobs(seed, max_square_size, fill, blob_size)]

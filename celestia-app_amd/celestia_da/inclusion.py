@@ -56,4 +56,61 @@ def create_commitment(blob: Blob, subtree_root_threshold: int = SUBTREE_ROOT_THR
     return create_commitments([blob], subtree_root_threshold, ctx)[0]
 
 
-__all__ = ["Blob", "create_commitment", "create_commitments", "_lib"]
+def sparse_shares_needed(sequence_len: int) -> int:
+    """shares.SparseSharesNeeded (first share 478 bytes, then 482)."""
+    if sequence_len == 0:
+        return 0
+    if sequence_len < 478:
+        return 1
+    return 1 + -(-(sequence_len - 478) // 482)
+
+
+def _round_up_pow2(x: int) -> int:
+    r = 1
+    while r < x:
+        r <<= 1
+    return r
+
+
+def blob_min_square_size(share_count: int) -> int:
+    """inclusion.BlobMinSquareSize."""
+    s = 0
+    while s * s < share_count:
+        s += 1
+    return _round_up_pow2(s)
+
+
+def sub_tree_width(share_count: int, subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD) -> int:
+    """inclusion.SubTreeWidth."""
+    s = -(-share_count // subtree_root_threshold)
+    return min(_round_up_pow2(s), blob_min_square_size(share_count))
+
+
+def merkle_mountain_range_sizes(total: int, max_tree: int):
+    """inclusion.MerkleMountainRangeSizes."""
+    sizes = []
+    while total:
+        if total >= max_tree:
+            s = max_tree
+        else:
+            s = 1
+            while s * 2 <= total:
+                s *= 2
+        sizes.append(s)
+        total -= s
+    return sizes
+
+
+def sha256_compressions(data_len: int, subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD) -> int:
+    """SHA-256 compressions of one CreateCommitment: 9 per leaf (0x00 || ns ||
+    share = 542 B), 3 per NMT inner node (181 B), 2 per RFC-6962 leaf (91 B)
+    and inner node (65 B)."""
+    n = sparse_shares_needed(data_len)
+    if n == 0:
+        return 0
+    sizes = merkle_mountain_range_sizes(n, sub_tree_width(n, subtree_root_threshold))
+    return 9 * n + 3 * sum(s - 1 for s in sizes) + 2 * len(sizes) + 2 * (len(sizes) - 1)
+
+
+__all__ = ["Blob", "create_commitment", "create_commitments", "sparse_shares_needed", "sub_tree_width",
+           "merkle_mountain_range_sizes", "blob_min_square_size", "sha256_compressions", "_lib"]

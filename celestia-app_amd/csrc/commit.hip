@@ -11,18 +11,20 @@
 //
 // MI355X mapping for a batch of blobs (plan: square_plan.cpp
 // plan_commitments):
-//   1. share writer (square.hip) lays every blob's sparse shares into one leaf
-//      array, blob starts aligned to their w, so all subtrees are perfect
-//      trees aligned to their size;
-//   2. leaf_kernel (nmt.hip) hashes every leaf (9 SHA-256 blocks of
-//      0x00 || ns || share -- the same leaves as the EDS Q0 cells);
+//   1. every blob's sparse shares get leaf positions in one array, blob starts
+//      aligned to their w, so all subtrees are perfect trees aligned to their
+//      size;
+//   2. blob_leaf_kernel hashes every leaf (9 SHA-256 blocks of
+//      0x00 || ns || share -- the same leaves as the EDS Q0 cells), building
+//      the share words straight from the blob bytes (no share copy in HBM);
 //   3. one subtree_level_kernel launch per level for ALL subtrees of ALL
-//      blobs: node n of level L covers leaves [n << L, (n + 1) << L); a binary
-//      search over the subtree table tells whether it lies inside a subtree
-//      tall enough (else the thread exits); a subtree's top node goes to its
-//      root slot;
-//   4. commitment_kernel: one workgroup per blob, RFC-6962 over its subtree
-//      roots in LDS (odd nodes promoted, which equals the RFC split rule).
+//      blobs: node n of level L covers leaves [n << L, (n + 1) << L); the
+//      per-leaf subtree table tells whether it lies inside a subtree tall
+//      enough (else the thread exits).
+//      A subtree's top node is hashed straight into its RFC-6962 leaf digest
+//      sha256(0x00 || root) (parallel, off the per-blob serial chain);
+//   4. commitment_kernel: one workgroup per blob, RFC-6962 inner levels over
+//      those digests in LDS (odd nodes promoted, equal to the RFC split rule).
 // VALU-bound like the EDS hashing: 9 compressions per share + 3 per inner node
 // + 2 per subtree root and RFC node.
 #include <cstring>
@@ -37,31 +39,178 @@ namespace {
 
 using square::Tree;
 
+// RFC-6962 leaf digest sha256(0x00 || root90) of a subtree root (I = the
+// root slot's big-endian words), stored as 8 state words: the commitment's
+// Merkle leaves are hashed where the roots are produced, in parallel, instead
+// of on the per-blob serial path.
+__device__ __forceinline__ void store_rfc_leaf(const uint32_t (&I)[kSlotWords], uint32_t* __restrict__ dig) {
+    uint32_t w[16];
+    ShaState st;
+    sha_init(st);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * q + j);
+        sha_compress(st, w);
+    }
+    uint4* d = reinterpret_cast<uint4*>(dig);
+    d[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+    d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+}
+
+// Leaf node of every blob share, hashed straight from the blob bytes (the
+// sparse share is never materialised).  Message = 0x00 || ns || share (542 B,
+// 9 blocks) with share = ns || info || [len BE32 if first] || data || zeros:
+//   words 0..14  namespace twice + info byte (from the segment record);
+//   word 15      first share: sequence length; continuation: data[0..3];
+//   words 16..   4 blob bytes each, from B + 4(t - 16) where B is the blob
+//                byte at message byte 64 (aligned dword loads + one v_perm
+//                per word: shift and byte swap together), bytes past the
+//                share's data masked to zero.
+__device__ __forceinline__ uint32_t data_word(uint32_t lo, uint32_t hi, uint32_t sel, int32_t v) {
+    const uint32_t x = __builtin_amdgcn_perm(hi, lo, sel);
+    if (v >= 4) return x;
+    if (v <= 0) return 0;
+    return x & (0xFFFFFFFFu << (32 - 8 * v));
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void blob_leaf_kernel(
+    const square::Segment* __restrict__ segs, const uint32_t* __restrict__ leaf_seg,
+    const uint8_t* __restrict__ data, uint8_t* __restrict__ slots, uint32_t n_leaves) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_leaves) return;
+    const square::Segment* g = segs + leaf_seg[i];
+    if (g->kind != square::kSegBlob) return;   // alignment gap: never read by a used node
+    const uint32_t j = i - g->start, len = g->len;
+    const bool first = j == 0;
+    const uint32_t dbase = first ? 0u : (kShare - kNs - 5) + (j - 1) * (kShare - kNs - 1);
+    const uint32_t cap = first ? kShare - kNs - 5 : kShare - kNs - 1;
+    const uint32_t cnt = min(len - dbase, cap);
+    const uint64_t B = g->src + dbase + (first ? 0 : 4);
+    const int32_t L = (int32_t)cnt - (first ? 0 : 4);   // valid bytes from B
+    const uint32_t sh = (uint32_t)(B & 3);
+    const uint32_t sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
+    // Dword indexes into `data` (batches < 16 GiB): A0 holds blob byte B; last
+    // = the dword holding the share's last data byte.  Loads are branch-free:
+    // each 4-dword chunk starts at min(chunk, last), so reads stay within 15
+    // bytes of the last data byte (callers give 16 B of slack after the
+    // buffer) and bytes past the data are masked by data_word.
+    const uint32_t A0 = (uint32_t)(B >> 2);
+    const uint32_t last = (uint32_t)(((int64_t)B + L - 1) >> 2);   // L >= -3 and B >= 4 when L <= 0
+    const uint32_t* D = reinterpret_cast<const uint32_t*>(data);
+    auto chunk = [&](uint32_t dw, uint32_t* x) {
+        dw = min(dw, last);
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] = D[dw + q];
+    };
+
+    uint32_t N[8];
+    {
+        const uint32_t* nsraw = reinterpret_cast<const uint32_t*>(g) + 7;   // Segment::ns at byte 28
+#pragma unroll
+        for (int k = 0; k < 8; k++) N[k] = bswap32(nsraw[k]);
+    }
+    const uint32_t info = (g->version << 1) | (first ? 1u : 0u);
+    uint32_t w[16];
+    w[0] = N[0] >> 8;
+#pragma unroll
+    for (int t = 1; t < 7; t++) w[t] = (N[t - 1] << 24) | (N[t] >> 8);
+    w[7] = (N[6] << 24) | ((N[7] >> 24) << 16) | (N[0] >> 16);
+#pragma unroll
+    for (int t = 8; t < 14; t++) w[t] = (N[t - 8] << 16) | (N[t - 7] >> 16);
+    w[14] = (N[6] << 16) | ((N[7] >> 24) << 8) | info;
+    // R = the 17 dwords block b reads (R[0] shared with block b - 1); the next
+    // block's 16 are loaded into X while the current block compresses.
+    auto load16 = [&](int b, uint32_t (&X)[16]) {
+        const uint32_t d0 = A0 + 16 * (b - 1) + 1;
+#pragma unroll
+        for (int c = 0; c < 4; c++) chunk(d0 + 4 * c, X + 4 * c);
+    };
+    uint32_t R0 = D[min(A0, last)], X[16];
+    if (first) {
+        w[15] = len;
+    } else {
+        const uint32_t Rm = D[A0 - 1];   // B - 4 >= the blob's first byte
+        w[15] = data_word(Rm, R0, sel, L + 4);
+    }
+    load16(1, X);
+    ShaState st;
+    sha_init(st);
+    sha_compress(st, w);
+#pragma unroll 1
+    for (int b = 1; b < 9; b++) {
+        uint32_t R[17];
+        R[0] = R0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) R[k + 1] = X[k];
+        if (b < 8) load16(b + 1, X);
+        const int32_t o = 64 * (b - 1);
+        if (b < 8) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = data_word(R[k], R[k + 1], sel, L - o - 4 * k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 7; k++) w[k] = data_word(R[k], R[k + 1], sel, L - o - 4 * k);
+            w[7] = data_word(R[7], R[8], sel, min(L - o - 28, 2)) | 0x8000u;   // message bytes 540..543
+#pragma unroll
+            for (int k = 8; k < 15; k++) w[k] = 0;
+            w[15] = kLeafMsgBits;
+        }
+        sha_compress(st, w);
+        R0 = R[16];
+    }
+    uint32_t out[kSlotWords];
+    N[7] &= 0xFF000000u;
+    leaf_node_words(N, st.h, out);
+    store_slot(slots + (size_t)i * kSlot, out);
+}
+
+// Per-leaf segment and subtree index tables, built on the device from the
+// plan's segment and subtree lists (binary search per leaf) instead of
+// shipping 8 bytes per leaf over PCIe.
+__global__ __launch_bounds__(256) void leaf_tables_kernel(const square::Segment* __restrict__ segs, uint32_t n_segs,
+                                                          const Tree* __restrict__ trees, uint32_t n_trees,
+                                                          uint32_t* __restrict__ leaf_seg,
+                                                          uint32_t* __restrict__ leaf_tree, uint32_t n_leaves) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_leaves) return;
+    uint32_t lo = 0, hi = n_segs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segs[mid].start <= i) lo = mid;
+        else hi = mid;
+    }
+    leaf_seg[i] = lo;
+    lo = 0;
+    hi = n_trees;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (trees[mid].off <= i) lo = mid;
+        else hi = mid;
+    }
+    leaf_tree[i] = lo;
+}
+
 // Height-0 subtrees (single share): the root is the leaf node itself.
 __global__ __launch_bounds__(256) void leaf_roots_kernel(const Tree* __restrict__ trees, uint32_t n_trees,
                                                          const uint8_t* __restrict__ leaf_slots,
-                                                         uint8_t* __restrict__ roots) {
+                                                         uint32_t* __restrict__ dig) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     if (t >= n_trees || trees[t].height != 0) return;
-    const uint4* s = reinterpret_cast<const uint4*>(leaf_slots + (size_t)trees[t].off * kSlot);
-    uint4* d = reinterpret_cast<uint4*>(roots + (size_t)t * kSlot);
-#pragma unroll
-    for (int q = 0; q < kSlot / 16; q++) d[q] = s[q];
+    uint32_t I[kSlotWords];
+    load_slot_be(leaf_slots + (size_t)trees[t].off * kSlot, I);
+    store_rfc_leaf(I, dig + (size_t)t * 8);
 }
 
 __global__ __launch_bounds__(256) void subtree_level_kernel(const Tree* __restrict__ trees, uint32_t n_trees,
+                                                            const uint32_t* __restrict__ leaf_tree,
                                                             const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                            uint8_t* __restrict__ roots, uint32_t level,
+                                                            uint32_t* __restrict__ dig, uint32_t level,
                                                             uint32_t n_nodes) {
     const uint32_t n = blockIdx.x * 256 + threadIdx.x;
     if (n >= n_nodes) return;
     const uint32_t leaf0 = n << level;
-    uint32_t lo = 0, hi = n_trees;   // last subtree with off <= leaf0
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (trees[mid].off <= leaf0) lo = mid;
-        else hi = mid;
-    }
+    const uint32_t lo = leaf_tree[leaf0];   // last subtree with off <= leaf0
     const Tree T = trees[lo];
     if (T.off > leaf0 || T.height < level || leaf0 - T.off >= (1u << T.height)) return;
     uint32_t L[kSlotWords], R[kSlotWords], w[16];
@@ -77,7 +226,13 @@ __global__ __launch_bounds__(256) void subtree_level_kernel(const Tree* __restri
     }
     uint32_t o[kSlotWords];
     inner_node_words(L, R, st.h, o);
-    store_slot(T.height == level ? roots + (size_t)lo * kSlot : out + (size_t)n * kSlot, o);
+    if (T.height == level) {   // subtree root -> its RFC-6962 leaf digest
+#pragma unroll
+        for (int t = 0; t < kSlotWords; t++) L[t] = bswap32(o[t]);
+        store_rfc_leaf(L, dig + (size_t)lo * 8);
+    } else {
+        store_slot(out + (size_t)n * kSlot, o);
+    }
 }
 
 __device__ __forceinline__ void rfc_inner(const uint32_t* a, const uint32_t* b, uint32_t* o) {
@@ -96,8 +251,10 @@ __device__ __forceinline__ void rfc_inner(const uint32_t* a, const uint32_t* b, 
     for (int j = 0; j < 8; j++) o[j] = st.h[j];
 }
 
-// One workgroup per blob: RFC-6962 root of its subtree roots.
-__global__ __launch_bounds__(256) void commitment_kernel(const uint8_t* __restrict__ roots,
+// One wave per blob: RFC-6962 root over its subtree roots' leaf digests (a
+// blob has at most a few hundred subtrees; the chain of levels is serial, so
+// a single wave per blob keeps every blob resident at once).
+__global__ __launch_bounds__(64) void commitment_kernel(const uint32_t* __restrict__ dig,
                                                          const uint32_t* __restrict__ blob_tree0, uint32_t max_trees,
                                                          uint8_t* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [max_trees][8] | [(max_trees+1)/2][8]
@@ -116,20 +273,7 @@ __global__ __launch_bounds__(256) void commitment_kernel(const uint8_t* __restri
     }
     uint32_t* src = hs;
     uint32_t* dst = hs + max_trees * 8;
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        uint32_t I[kSlotWords], w[16];
-        load_slot_be(roots + (size_t)(t0 + i) * kSlot, I);
-        ShaState st;
-        sha_init(st);
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * q + j);
-            sha_compress(st, w);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) src[i * 8 + j] = st.h[j];
-    }
+    for (uint32_t i = threadIdx.x; i < m * 8; i += blockDim.x) src[i] = dig[(size_t)t0 * 8 + i];
     __syncthreads();
     while (m > 1) {
         const uint32_t pairs = m / 2;
@@ -182,28 +326,27 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
     const uint32_t* d_bt = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b + tree_b);
     const uint32_t N = p.n_leaves, n_trees = (uint32_t)p.trees.size();
     if (N) {
-        if ((rc = check(cm_shares_.ensure((size_t)N * kShare), "hipMalloc"))) return rc;
         if ((rc = check(cm_leaf_.ensure((size_t)N * kSlot), "hipMalloc"))) return rc;
         if ((rc = check(cm_lvl_.ensure((size_t)(N / 2 + 1) * kSlot), "hipMalloc"))) return rc;
-        if ((rc = check(cm_roots_.ensure((size_t)n_trees * kSlot), "hipMalloc"))) return rc;
-        if ((rc = check(err_buf_.ensure(4), "hipMalloc"))) return rc;
-        if ((rc = check(launch_share_writer(d_segs, (uint32_t)p.segs.size(), nullptr, d_data, cm_shares_.as<uint8_t>(),
-                                            N, s),
-                        "share writer")))
-            return rc;
-        const CellGrid g{cm_shares_.as<uint8_t>(), 0, 1, N, N, 0, 0, 0xFFFFFFFFu};
-        if ((rc = check(launch_leaves(g, 1, cm_leaf_.as<uint8_t>(), err_buf_.as<uint32_t>(), false, false, s),
-                        "leaves")))
-            return rc;
+        if ((rc = check(cm_roots_.ensure((size_t)n_trees * 32), "hipMalloc"))) return rc;   // RFC leaf digests
+        if ((rc = check(cm_tables_.ensure((size_t)N * 8), "hipMalloc"))) return rc;
+        uint32_t* d_leaf_seg = cm_tables_.as<uint32_t>();
+        uint32_t* d_leaf_tree = d_leaf_seg + N;
+        hipLaunchKernelGGL(leaf_tables_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, (uint32_t)p.segs.size(),
+                           d_trees, n_trees, d_leaf_seg, d_leaf_tree, N);
+        if ((rc = check(hipGetLastError(), "leaf tables"))) return rc;
+        hipLaunchKernelGGL(blob_leaf_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, d_leaf_seg, d_data,
+                           cm_leaf_.as<uint8_t>(), N);
+        if ((rc = check(hipGetLastError(), "blob leaves"))) return rc;
         hipLaunchKernelGGL(leaf_roots_kernel, dim3((n_trees + 255) / 256), dim3(256), 0, s, d_trees, n_trees,
-                           cm_leaf_.as<uint8_t>(), cm_roots_.as<uint8_t>());
+                           cm_leaf_.as<uint8_t>(), cm_roots_.as<uint32_t>());
         if ((rc = check(hipGetLastError(), "leaf roots"))) return rc;
         for (uint32_t L = 1; L <= p.max_height; L++) {
             uint8_t* in = (L - 1) % 2 == 0 ? cm_leaf_.as<uint8_t>() : cm_lvl_.as<uint8_t>();
             uint8_t* out = L % 2 == 0 ? cm_leaf_.as<uint8_t>() : cm_lvl_.as<uint8_t>();
             const uint32_t n_nodes = (uint32_t)(((uint64_t)N + (1ull << L) - 1) >> L);
-            hipLaunchKernelGGL(subtree_level_kernel, dim3((n_nodes + 255) / 256), dim3(256), 0, s, d_trees, n_trees, in,
-                               out, cm_roots_.as<uint8_t>(), L, n_nodes);
+            hipLaunchKernelGGL(subtree_level_kernel, dim3((n_nodes + 255) / 256), dim3(256), 0, s, d_trees, n_trees,
+                               d_leaf_tree, in, out, cm_roots_.as<uint32_t>(), L, n_nodes);
             if ((rc = check(hipGetLastError(), "subtree level"))) return rc;
         }
     }
@@ -215,7 +358,7 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                     "hipFuncSetAttribute")))
         return rc;
-    hipLaunchKernelGGL(commitment_kernel, dim3(n_blobs), dim3(256), lds, s, cm_roots_.as<uint8_t>(), d_bt, mt, d_out);
+    hipLaunchKernelGGL(commitment_kernel, dim3(n_blobs), dim3(64), lds, s, cm_roots_.as<uint32_t>(), d_bt, mt, d_out);
     return check(hipGetLastError(), "commitments");
 }
 

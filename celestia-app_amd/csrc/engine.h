@@ -15,8 +15,10 @@
 namespace cda {
 
 // square.hip: writes n_shares shares of a square::Plan / CommitPlan layout.
-hipError_t launch_share_writer(const square::Segment* segs, uint32_t n_segs, const uint8_t* compact,
-                               const uint8_t* txs, uint8_t* ods, uint32_t n_shares, hipStream_t s);
+// hint (optional): segment index of every kHintShares-th share.
+hipError_t launch_share_writer(const square::Segment* segs, uint32_t n_segs, const uint32_t* hint,
+                               const uint8_t* compact, const uint8_t* txs, uint8_t* ods, uint32_t n_shares,
+                               hipStream_t s);
 
 struct DevBuf {
     void* ptr = nullptr;
@@ -134,7 +136,7 @@ class Engine {
     // square construction: device plan (segments + compact shares), device
     // copy of host txs, pinned staging for the plan and its copy-done event
     DevBuf sq_plan_, sq_txs_;
-    DevBuf cm_plan_, cm_shares_, cm_leaf_, cm_lvl_, cm_roots_, cm_out_;   // commitments
+    DevBuf cm_plan_, cm_tables_, cm_leaf_, cm_lvl_, cm_roots_, cm_out_;   // commitments
     void* sq_stage_ = nullptr;
     size_t sq_stage_bytes_ = 0;
     hipEvent_t sq_event_ = nullptr;

@@ -28,17 +28,24 @@ namespace {
 using square::Segment;
 
 __global__ __launch_bounds__(256) void share_writer_kernel(const Segment* __restrict__ segs, uint32_t n_segs,
+                                                           const uint32_t* __restrict__ hint,
                                                            const uint8_t* __restrict__ compact,
                                                            const uint8_t* __restrict__ txs, uint8_t* __restrict__ ods,
                                                            uint32_t n_shares) {
     const uint32_t s = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     if (s >= n_shares) return;
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t lo = 0, hi = n_segs;   // last segment with start <= s
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (segs[mid].start <= s) lo = mid;
-        else hi = mid;
+    uint32_t lo = 0;   // last segment with start <= s
+    if (hint) {        // segment of share (s / kHintShares) * kHintShares, then a short forward scan
+        lo = hint[s / square::kHintShares];
+        while (lo + 1 < n_segs && segs[lo + 1].start <= s) lo++;
+    } else {
+        uint32_t hi = n_segs;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (segs[mid].start <= s) lo = mid;
+            else hi = mid;
+        }
     }
     const Segment& g = segs[lo];
     const uint32_t j = s - g.start;
@@ -96,11 +103,11 @@ __global__ __launch_bounds__(256) void share_writer_kernel(const Segment* __rest
 
 }  // namespace
 
-hipError_t launch_share_writer(const Segment* segs, uint32_t n_segs, const uint8_t* compact, const uint8_t* txs,
-                               uint8_t* ods, uint32_t n_shares, hipStream_t s) {
+hipError_t launch_share_writer(const Segment* segs, uint32_t n_segs, const uint32_t* hint, const uint8_t* compact,
+                               const uint8_t* txs, uint8_t* ods, uint32_t n_shares, hipStream_t s) {
     if (n_shares == 0 || n_segs == 0) return hipSuccess;
-    hipLaunchKernelGGL(share_writer_kernel, dim3((n_shares + 3) / 4), dim3(256), 0, s, segs, n_segs, compact, txs, ods,
-                       n_shares);
+    hipLaunchKernelGGL(share_writer_kernel, dim3((n_shares + 3) / 4), dim3(256), 0, s, segs, n_segs, hint, compact, txs,
+                       ods, n_shares);
     return hipGetLastError();
 }
 
@@ -129,8 +136,8 @@ int Engine::enqueue_square(const square::Plan& p, const uint8_t* d_txs, uint8_t*
     if ((rc = check(hipMemcpyAsync(sq_plan_.ptr, sq_stage_, plan_b, hipMemcpyHostToDevice, s), "H2D plan"))) return rc;
     if ((rc = check(hipEventRecord(sq_event_, s), "hipEventRecord"))) return rc;
     const uint32_t n_shares = p.square_size * p.square_size;
-    return check(launch_share_writer(sq_plan_.as<Segment>(), (uint32_t)p.segs.size(), sq_plan_.as<uint8_t>() + seg_b,
-                                     d_txs, d_ods, n_shares, s),
+    return check(launch_share_writer(sq_plan_.as<Segment>(), (uint32_t)p.segs.size(), nullptr,
+                                     sq_plan_.as<uint8_t>() + seg_b, d_txs, d_ods, n_shares, s),
                  "share writer");
 }
 

@@ -58,6 +58,9 @@ struct Plan {
 
 enum Mode { kConstruct = 0, kBuild = 1 };
 
+// Share-writer hint granularity: hint[i] = segment holding share i * kHintShares.
+constexpr uint32_t kHintShares = 16;
+
 // Plans the square for n txs (tx i = txs[off[i], off[i+1])).  Returns 0, or -1
 // with the go-square error text in *err.
 int plan(const uint8_t* txs, const uint64_t* off, uint32_t n, uint32_t max_square_size, uint32_t threshold, Mode mode,
