@@ -3,8 +3,8 @@
 Host-side mirror of the reference's Go API (pkg/da, pkg/wrapper, rsmt2d,
 go-square square) over the C ABI of libcda.so (include/cda.h).  See DESIGN.md.
 """
-from . import _lib, blobfactory, da, inclusion, rsmt2d, square, wrapper  # noqa: F401
+from . import _lib, blobfactory, da, inclusion, proof, rsmt2d, square, wrapper  # noqa: F401
 from ._lib import CdaError, Context, PushOrderError, SquareError, default_context, load  # noqa: F401
 
-__all__ = ["da", "rsmt2d", "wrapper", "square", "inclusion", "blobfactory", "Context", "CdaError", "PushOrderError", "SquareError",
+__all__ = ["da", "rsmt2d", "wrapper", "square", "inclusion", "proof", "blobfactory", "Context", "CdaError", "PushOrderError", "SquareError",
            "default_context", "load"]

@@ -41,6 +41,8 @@ EXPORTED = (
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
     "cda_blob_commitments", "cda_blob_commitments_device",
+    "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
+    "cda_square_blob_commitments",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -112,6 +114,13 @@ def load():
                                                   vp, C.c_size_t, u32p, u32p, u32p, vp]
         L.cda_blob_commitments.argtypes = [ctxp, u8p, u8p, u64p, u8p, C.c_uint32, C.c_uint32, u8p]
         L.cda_blob_commitments_device.argtypes = [ctxp, u8p, u64p, u8p, C.c_uint32, C.c_uint32, vp, vp, vp]
+        i32p = C.POINTER(C.c_int32)
+        L.cda_square_create.argtypes = [ctxp, u8p, C.c_uint32, C.POINTER(vp)]
+        L.cda_square_destroy.argtypes = [vp]
+        L.cda_square_dah.argtypes = [vp, u32p, u8p, u8p, u8p, u8p]
+        L.cda_square_share_proof.argtypes = [vp, C.c_uint32, C.c_uint32, u8p, u32p, u32p, i32p, i32p, u32p, u8p,
+                                             u8p, u8p, u8p]
+        L.cda_square_blob_commitments.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint32, u8p]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L

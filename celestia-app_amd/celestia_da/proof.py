@@ -1,0 +1,141 @@
+"""Mirror of pkg/proof (ShareProof, NewShareInclusionProofFromEDS) and
+pkg/inclusion GetCommitment over a device-resident square (libcda.so).
+
+Reference: pkg/proof/proof.go:77-206, pkg/proof/proof.pb.go (ShareProof,
+RowProof, NMTProof, Proof field names), pkg/inclusion/get_commit.go:12-30.
+The square is extended once (`ResidentSquare`); the EDS, every row-tree
+level and the data-root tree stay in HBM, so each proof is a gather.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import NMT_ROOT_SIZE, SHARE_SIZE, default_context, ptr
+
+
+@dataclass
+class NMTProof:                     # proof.pb.go NMTProof
+    start: int
+    end: int
+    nodes: list
+    leaf_hash: bytes = b""
+
+
+@dataclass
+class Proof:                        # go-square/merkle Proof (RowProof.Proofs)
+    total: int
+    index: int
+    leaf_hash: bytes
+    aunts: list
+
+
+@dataclass
+class RowProof:
+    row_roots: list
+    proofs: list
+    start_row: int
+    end_row: int
+
+
+@dataclass
+class ShareProof:
+    data: list
+    share_proofs: list
+    namespace_id: bytes
+    row_proof: RowProof
+    namespace_version: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+def _log2(x: int) -> int:
+    n = 0
+    while (1 << n) < x:
+        n += 1
+    return n
+
+
+class ResidentSquare:
+    """An extended square kept on the GPU (cda_square_*)."""
+
+    def __init__(self, ods, ctx=None):
+        self.ctx = ctx or default_context()
+        a = np.ascontiguousarray(np.asarray(ods, dtype=np.uint8).reshape(-1, SHARE_SIZE))
+        self.h = C.c_void_p()
+        rc = self.ctx.lib.cda_square_create(self.ctx.h, ptr(a), a.shape[0], C.byref(self.h))
+        self.push_order_error = rc == _lib.CDA_ERR_PUSH_ORDER
+        if rc not in (_lib.CDA_OK, _lib.CDA_ERR_PUSH_ORDER):
+            self.ctx.check(rc)
+        k = C.c_uint32()
+        self.ctx.check(self.ctx.lib.cda_square_dah(self.h, C.byref(k), None, None, None, None))
+        self.k = k.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.cda_square_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def dah(self):
+        """(row_roots, col_roots, data_root)."""
+        W = 2 * self.k
+        rows = np.empty(W * NMT_ROOT_SIZE, dtype=np.uint8)
+        cols = np.empty(W * NMT_ROOT_SIZE, dtype=np.uint8)
+        root = np.empty(32, dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.cda_square_dah(self.h, None, ptr(rows), ptr(cols), ptr(root), None))
+        split = lambda b: [b[i * NMT_ROOT_SIZE:(i + 1) * NMT_ROOT_SIZE].tobytes() for i in range(W)]  # noqa: E731
+        return split(rows), split(cols), root.tobytes()
+
+    def eds(self) -> np.ndarray:
+        W = 2 * self.k
+        out = np.empty(W * W * SHARE_SIZE, dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.cda_square_dah(self.h, None, None, None, None, ptr(out)))
+        return out.reshape(W, W, SHARE_SIZE)
+
+    def share_proof(self, namespace: bytes, start: int, end: int) -> ShareProof:
+        """proof.NewShareInclusionProofFromEDS(eds, namespace, shares.Range{start, end})."""
+        k = self.k
+        if not (0 <= start < end <= k * k):
+            raise _lib.CdaError(_lib.CDA_ERR_INVALID, "share range out of the original square")
+        W = 2 * k
+        R = (end - 1) // k - start // k + 1
+        M, A = 2 * _log2(W), _log2(2 * W)
+        shares = np.empty((end - start) * SHARE_SIZE, dtype=np.uint8)
+        ns, ne = (C.c_int32 * R)(), (C.c_int32 * R)()
+        cnt = (C.c_uint32 * R)()
+        nodes = np.empty(R * M * NMT_ROOT_SIZE, dtype=np.uint8)
+        roots = np.empty(R * NMT_ROOT_SIZE, dtype=np.uint8)
+        leaf = np.empty(R * 32, dtype=np.uint8)
+        aunts = np.empty(R * A * 32, dtype=np.uint8)
+        r0, r1 = C.c_uint32(), C.c_uint32()
+        self.ctx.check(self.ctx.lib.cda_square_share_proof(self.h, start, end, ptr(shares), C.byref(r0), C.byref(r1),
+                                                           ns, ne, cnt, ptr(nodes), ptr(roots), ptr(leaf),
+                                                           ptr(aunts)))
+        nb, rb, lb, ab = nodes.tobytes(), roots.tobytes(), leaf.tobytes(), aunts.tobytes()
+        sp = [NMTProof(ns[i], ne[i], [nb[(i * M + q) * 90:(i * M + q + 1) * 90] for q in range(cnt[i])])
+              for i in range(R)]
+        proofs = [Proof(2 * W, r0.value + i, lb[32 * i:32 * (i + 1)],
+                        [ab[(i * A + q) * 32:(i * A + q + 1) * 32] for q in range(A)]) for i in range(R)]
+        sb = shares.tobytes()
+        return ShareProof(data=[sb[i * SHARE_SIZE:(i + 1) * SHARE_SIZE] for i in range(end - start)],
+                          share_proofs=sp, namespace_id=bytes(namespace[1:]),
+                          row_proof=RowProof([rb[90 * i:90 * (i + 1)] for i in range(R)], proofs, r0.value, r1.value),
+                          namespace_version=namespace[0])
+
+    def blob_commitments(self, starts, share_lens, subtree_root_threshold: int = 64):
+        """inclusion.GetCommitment for each (start, share_len)."""
+        n = len(starts)
+        s = (C.c_uint32 * max(1, n))(*starts)
+        ln = (C.c_uint32 * max(1, n))(*share_lens)
+        out = np.empty(32 * max(1, n), dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.cda_square_blob_commitments(self.h, s, ln, n, subtree_root_threshold, ptr(out)))
+        b = out.tobytes()
+        return [b[32 * i:32 * (i + 1)] for i in range(n)]

@@ -14,6 +14,11 @@ struct cda_ctx {
     explicit cda_ctx(int dev) : eng(dev) {}
 };
 
+struct cda_square {
+    cda_ctx* ctx;
+    cda::ResidentSquare sq;
+};
+
 namespace {
 
 // pkg/da/data_availability_header.go SquareSize + IsPowerOfTwo
@@ -351,6 +356,70 @@ int cda_blob_commitments_device(cda_ctx* ctx, const uint8_t* namespaces, const u
         hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_commitments(p, n, static_cast<const uint8_t*>(d_data), static_cast<uint8_t*>(d_commitments),
                                      s);
+    });
+}
+
+int cda_square_create(cda_ctx* ctx, const uint8_t* ods, uint32_t n_shares, cda_square** out) {
+    if (!out) return CDA_ERR_INVALID;
+    *out = nullptr;
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        uint32_t k;
+        if (!square_width(n_shares, &k)) return not_pow2(e, n_shares);
+        if (!ods) return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda_square* h = new cda_square{ctx, {}};
+        const int rc = e.square_create(ods, k, &h->sq);
+        if (rc != CDA_OK && rc != CDA_ERR_PUSH_ORDER) {
+            delete h;
+            return rc;
+        }
+        *out = h;   // a push-order failure still leaves the EDS (as ExtendShares does)
+        return rc;
+    });
+}
+
+int cda_square_destroy(cda_square* sq) {
+    if (!sq) return CDA_OK;
+    std::lock_guard<std::mutex> g(sq->ctx->eng.mutex());
+    delete sq;
+    return CDA_OK;
+}
+
+int cda_square_dah(cda_square* sq, uint32_t* k, uint8_t* row_roots, uint8_t* col_roots, uint8_t* data_root,
+                   uint8_t* eds) {
+    if (!sq) return CDA_ERR_INVALID;
+    return guarded(sq->ctx, [&](cda::Engine& e) -> int {
+        if (k) *k = sq->sq.k;
+        int rc;
+        if (row_roots && (rc = e.square_read(&sq->sq, cda::ResidentSquare::kRowRoots, row_roots))) return rc;
+        if (col_roots && (rc = e.square_read(&sq->sq, cda::ResidentSquare::kColRoots, col_roots))) return rc;
+        if (data_root && (rc = e.square_read(&sq->sq, cda::ResidentSquare::kDataRoot, data_root))) return rc;
+        if (eds && (rc = e.square_read(&sq->sq, cda::ResidentSquare::kEds, eds))) return rc;
+        return CDA_OK;
+    });
+}
+
+int cda_square_share_proof(cda_square* sq, uint32_t start, uint32_t end, uint8_t* shares, uint32_t* start_row,
+                           uint32_t* end_row, int32_t* nmt_start, int32_t* nmt_end, uint32_t* nmt_count,
+                           uint8_t* nmt_nodes, uint8_t* row_roots, uint8_t* row_leaf_hash, uint8_t* row_aunts) {
+    if (!sq) return CDA_ERR_INVALID;
+    return guarded(sq->ctx, [&](cda::Engine& e) -> int {
+        if (!nmt_start || !nmt_end || !nmt_count || !start_row || !end_row)
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        cda::Engine::ShareProofOut o{shares, 0, 0, nmt_start, nmt_end, nmt_count, nmt_nodes, row_roots,
+                                     row_leaf_hash, row_aunts};
+        const int rc = e.square_share_proof(&sq->sq, start, end, &o);
+        *start_row = o.start_row;
+        *end_row = o.end_row;
+        return rc;
+    });
+}
+
+int cda_square_blob_commitments(cda_square* sq, const uint32_t* starts, const uint32_t* share_lens, uint32_t n,
+                                uint32_t threshold, uint8_t* commitments) {
+    if (!sq) return CDA_ERR_INVALID;
+    return guarded(sq->ctx, [&](cda::Engine& e) -> int {
+        if (n && (!starts || !share_lens || !commitments)) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.square_blob_commitments(&sq->sq, starts, share_lens, n, threshold, commitments);
     });
 }
 

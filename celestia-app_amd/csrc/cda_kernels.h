@@ -106,6 +106,8 @@ hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_
 // <= 4096).
 hipError_t launch_data_root_slots(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares,
                                   uint32_t* digests, uint8_t* data_roots, hipStream_t stream);
+// RFC-6962 leaf digests sha256(0x00 || slot[0:90]) of n slots (8 words each).
+hipError_t launch_rfc_leaves(const uint8_t* slots, uint32_t n, uint32_t* digests, hipStream_t stream);
 hipError_t launch_data_root_digests(const uint32_t* digests, uint32_t n_items, uint32_t n_squares,
                                     uint8_t* data_roots, hipStream_t stream);
 // Pack n_slots 96-B root slots (rows then columns) into 90-B roots.

@@ -291,7 +291,32 @@ __global__ __launch_bounds__(64) void commitment_kernel(const uint32_t* __restri
     }
 }
 
+// RFC-6962 leaf digests of n 96-B slots.
+__global__ __launch_bounds__(256) void slot_digest_kernel(const uint8_t* __restrict__ slots, uint32_t n,
+                                                          uint32_t* __restrict__ dig) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= n) return;
+    uint32_t I[kSlotWords];
+    load_slot_be(slots + (size_t)t * kSlot, I);
+    store_rfc_leaf(I, dig + (size_t)t * 8);
+}
+
 }  // namespace
+
+hipError_t launch_slot_merkle_roots(const uint8_t* slots, const uint32_t* bt, uint32_t n_sets, uint32_t n_slots,
+                                    uint32_t max_n, uint32_t* dig, uint8_t* out, hipStream_t s) {
+    if (n_sets == 0) return hipSuccess;
+    if (n_slots) {
+        hipLaunchKernelGGL(slot_digest_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, s, slots, n_slots, dig);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    const uint32_t mt = max_n ? max_n : 1;
+    const size_t lds = (size_t)(mt + (mt + 1) / 2) * 32;
+    if (lds > 64 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(commitment_kernel, dim3(n_sets), dim3(64), lds, s, dig, bt, mt, out);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------
 // Engine glue

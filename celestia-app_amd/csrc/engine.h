@@ -29,6 +29,30 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(ptr); }
 };
 
+// commit.hip: RFC-6962 root (merkle.HashFromByteSlices) of each set of 96-B
+// node slots: set b = slots [bt[b], bt[b+1]) (bt in device memory, n_sets + 1
+// entries, at most max_n per set); dig = scratch, 8 words per slot.
+hipError_t launch_slot_merkle_roots(const uint8_t* slots, const uint32_t* bt, uint32_t n_sets, uint32_t n_slots,
+                                    uint32_t max_n, uint32_t* dig, uint8_t* out, hipStream_t s);
+
+// A square kept in HBM after extension (proof.hip): the EDS, every level of
+// every row tree (level 0 = the W x W leaf slots, level L = [W][W >> L] 96-B
+// slots), the roots and all RFC-6962 levels of the data-root tree.
+struct ResidentSquare {
+    enum Part { kRowRoots, kColRoots, kDataRoot, kEds };
+    uint32_t k = 0, log_w = 0, push_err = 0xFFFFFFFFu;
+    DevBuf eds, levels, col_a, col_b, roots_slots, rfc, rows, cols, root, err, scratch, pieces;
+    uint64_t level_offset(uint32_t L) const;
+    ~ResidentSquare();
+};
+// One copy out of a resident square (byte offsets into the named buffer).
+struct GatherPiece {
+    enum Buf : uint32_t { kEds = 0, kLevels = 1, kRfc = 2, kRows = 3, kRootSlots = 4 };
+    uint32_t buf;
+    uint64_t src, dst;
+    uint32_t len;
+};
+
 class Engine {
   public:
     explicit Engine(int device);
@@ -86,6 +110,26 @@ class Engine {
                             hipStream_t s);
     int host_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* data, size_t data_len,
                          uint8_t* out);
+
+    // Resident squares and proofs (proof.hip).
+    int square_create(const uint8_t* ods, uint32_t k, ResidentSquare* sq);
+    int square_gather(ResidentSquare* sq, const std::vector<GatherPiece>& pieces, uint8_t* out, size_t out_len);
+    int square_gather_device(ResidentSquare* sq, const std::vector<GatherPiece>& pieces, size_t out_len);
+    int square_read(ResidentSquare* sq, ResidentSquare::Part part, uint8_t* out);   // synchronous D2H
+    struct ShareProofOut {
+        uint8_t* shares;
+        uint32_t start_row, end_row;
+        int32_t* nmt_start;
+        int32_t* nmt_end;
+        uint32_t* nmt_count;
+        uint8_t* nmt_nodes;       // [rows][2 log2(2k)][90]
+        uint8_t* row_roots;       // [rows][90]
+        uint8_t* row_leaf_hash;   // [rows][32]
+        uint8_t* row_aunts;       // [rows][log2(4k)][32]
+    };
+    int square_share_proof(ResidentSquare* sq, uint32_t start, uint32_t end, ShareProofOut* out);
+    int square_blob_commitments(ResidentSquare* sq, const uint32_t* starts, const uint32_t* lens, uint32_t n,
+                                uint32_t threshold, uint8_t* out);
 
     // Stage timing with HIP events on the launch stream (bench / profiling).
     enum Stage { kStageRsQ0 = 0, kStageRsQ3, kStageOrder, kStageLeaves, kStageLevels, kStageDataRoot, kNumStages };

@@ -438,6 +438,12 @@ hipError_t launch_data_root_slots(const uint8_t* root_slots, uint32_t n_items, u
     return launch_data_root_digests(dig, n_items, n, data_roots, s);
 }
 
+hipError_t launch_rfc_leaves(const uint8_t* slots, uint32_t n, uint32_t* dig, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rfc_leaf_kernel, dim3((n + 255) / 256), dim3(256), 0, s, slots, n, dig);
+    return hipGetLastError();
+}
+
 hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint32_t n, uint8_t* data_roots,
                                     hipStream_t s) {
     if (n_items < 2 || n_items > 4096 || (n_items & (n_items - 1))) return hipErrorInvalidValue;

@@ -26,6 +26,11 @@
  *                          go-square square.Construct / square.Build (EXT
  *                          v1.1.0, go.mod:9; app/process_proposal.go:122,
  *                          app/prepare_proposal.go:50, app/extend_block.go:16)
+ *   cda_blob_commitments   go-square inclusion.CreateCommitment
+ *                          (x/blob/types/blob_tx.go:98, payforblob.go:53)
+ *   cda_square_*           resident squares: proof.NewShareInclusionProofFromEDS
+ *                          (pkg/proof/proof.go:77), inclusion.GetCommitment
+ *                          (pkg/inclusion/get_commit.go:12)
  *
  * Conventions
  *   - All buffers are plain byte arrays; shares are row-major and contiguous
@@ -220,6 +225,39 @@ int cda_blob_commitments(cda_ctx *ctx, const uint8_t *namespaces, const uint8_t 
 int cda_blob_commitments_device(cda_ctx *ctx, const uint8_t *namespaces, const uint64_t *data_off,
                                 const uint8_t *share_versions, uint32_t n, uint32_t threshold, const void *d_data,
                                 void *d_commitments, void *stream);
+
+/* ---- Resident squares: NMT proofs and commitments from cached nodes -------
+ * (SURVEY.md 8(f) row 3).  cda_square_create extends one ODS and keeps in HBM
+ * the EDS, every level of every row tree (the reference's
+ * EDSSubTreeRootCacher, pkg/inclusion/nmt_caching.go:80-124) and all levels
+ * of the data-root tree, so proofs are index arithmetic plus one gather.
+ * On CDA_ERR_PUSH_ORDER the handle is still created (the EDS exists). */
+typedef struct cda_square cda_square;
+int cda_square_create(cda_ctx *ctx, const uint8_t *ods, uint32_t n_shares, cda_square **out);
+int cda_square_destroy(cda_square *sq);
+/* Any output may be NULL: k, row/col roots (2k*90 each), data root (32), EDS ((2k)^2*512). */
+int cda_square_dah(cda_square *sq, uint32_t *k, uint8_t *row_roots, uint8_t *col_roots, uint8_t *data_root,
+                   uint8_t *eds);
+/* proof.NewShareInclusionProofFromEDS (pkg/proof/proof.go:77-145) for the ODS
+ * share range [start, end) (row-major ODS indexes), R = end_row - start_row + 1
+ * rows, A = log2(4k) aunts, M = 2*log2(2k) node slots per row:
+ *   shares        (end - start) * 512: ShareProof.Data, concatenated
+ *   nmt_start/end R entries: NMTProof.Start / End (leaf range in the row)
+ *   nmt_count     R entries; nmt_nodes R*M*90 B: NMTProof.Nodes of row i at
+ *                 [i*M*90, ...) (nmt ProveRange order: maximal subtrees outside
+ *                 the range, left to right); NMTProof.LeafHash is empty
+ *   row_roots     R*90: RowProof.RowRoots
+ *   row_leaf_hash R*32, row_aunts R*A*32: RowProof.Proofs (merkle proofs of
+ *                 the rows among rowRoots || colRoots: Total 4k, Index = row,
+ *                 LeafHash, Aunts bottom-up) */
+int cda_square_share_proof(cda_square *sq, uint32_t start, uint32_t end, uint8_t *shares, uint32_t *start_row,
+                           uint32_t *end_row, int32_t *nmt_start, int32_t *nmt_end, uint32_t *nmt_count,
+                           uint8_t *nmt_nodes, uint8_t *row_roots, uint8_t *row_leaf_hash, uint8_t *row_aunts);
+/* inclusion.GetCommitment (pkg/inclusion/get_commit.go:12-30) for n blobs:
+ * blob i starts at ODS share starts[i] (normalised by NextShareIndex as the
+ * reference does) and spans share_lens[i] shares; commitments n*32. */
+int cda_square_blob_commitments(cda_square *sq, const uint32_t *starts, const uint32_t *share_lens, uint32_t n,
+                                uint32_t threshold, uint8_t *commitments);
 
 /* Stage timing (HIP events on the launch stream).  When enabled, every
  * enqueued stage is bracketed by events; cda_stage_times synchronises them and
