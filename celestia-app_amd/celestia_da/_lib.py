@@ -30,6 +30,8 @@ CDA_ERR_OOM = -5
 CDA_ERR_INVALID = -6
 CDA_ERR_UNSUPPORTED = -7
 CDA_ERR_SQUARE = -8
+CDA_ERR_BYZANTINE = -9
+CDA_ERR_UNREPAIRABLE = -10
 
 CDA_SQUARE_CONSTRUCT = 0
 CDA_SQUARE_BUILD = 1
@@ -42,7 +44,7 @@ EXPORTED = (
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
     "cda_blob_commitments", "cda_blob_commitments_device",
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
-    "cda_square_blob_commitments",
+    "cda_square_blob_commitments", "cda_repair", "cda_rs_decode",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -55,6 +57,19 @@ class CdaError(RuntimeError):
 
 class PushOrderError(CdaError):
     """nmt ErrInvalidPushOrder surfaced through RowRoots/ColRoots."""
+
+
+class ByzantineDataError(CdaError):
+    """rsmt2d ErrByzantineData: axis 0 (row) / 1 (col) and index of the
+    first vector whose rebuilt cells contradict its root or encoding."""
+
+    def __init__(self, rc: int, msg: str, axis: int = -1, index: int = 0):
+        super().__init__(rc, msg)
+        self.axis, self.index = axis, index
+
+
+class UnrepairableError(CdaError):
+    """rsmt2d ErrUnrepairableDataSquare / reedsolomon ErrTooFewShards."""
 
 
 class SquareError(CdaError):
@@ -121,6 +136,8 @@ def load():
         L.cda_square_share_proof.argtypes = [vp, C.c_uint32, C.c_uint32, u8p, u32p, u32p, i32p, i32p, u32p, u8p,
                                              u8p, u8p, u8p]
         L.cda_square_blob_commitments.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint32, u8p]
+        L.cda_repair.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
+        L.cda_rs_decode.argtypes = [ctxp, u8p, u8p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L
@@ -164,6 +181,10 @@ class Context:
             raise PushOrderError(rc, msg)
         if rc == CDA_ERR_SQUARE:
             raise SquareError(rc, msg)
+        if rc == CDA_ERR_BYZANTINE:
+            raise ByzantineDataError(rc, msg)
+        if rc == CDA_ERR_UNREPAIRABLE:
+            raise UnrepairableError(rc, msg)
         raise CdaError(rc, msg)
 
     def set_profiling(self, on: bool):

@@ -8,14 +8,20 @@ through libcda.so.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
 from . import _lib
-from ._lib import SHARE_SIZE, CdaError, PushOrderError, default_context, ptr
+from ._lib import SHARE_SIZE, ByzantineDataError, CdaError, PushOrderError, UnrepairableError, default_context, ptr
 
 ROW = 0
 COL = 1
 LEOPARD = "Leopard"
+
+
+ErrByzantineData = ByzantineDataError
+ErrUnrepairableDataSquare = UnrepairableError
 
 
 class ErrUnevenChunks(ValueError):
@@ -66,6 +72,26 @@ class LeoRSCodec:
         parity = np.empty_like(cw)
         self.ctx.check(self.ctx.lib.cda_rs_encode(self.ctx.h, ptr(cw), k, L, n, ptr(parity)))
         return parity
+
+    def decode(self, data):
+        """Codec.Decode (reedsolomon Reconstruct): 2k shards, missing ones as
+        None; returns all 2k shards (ErrTooFewShards -> UnrepairableError)."""
+        data = list(data)
+        n = len(data)
+        present = np.array([d is not None for d in data], dtype=np.uint8)
+        size = next((len(d) for d in data if d is not None), 0)
+        filled = _as_shares([d if d is not None else bytes(size) for d in data])
+        self.decode_batch(filled[None], present[None])
+        return [filled[i].tobytes() for i in range(n)]
+
+    def decode_batch(self, shards: np.ndarray, present: np.ndarray) -> np.ndarray:
+        """Reconstruct, in place, n codewords (n, 2k, L) with presence (n, 2k)."""
+        n, w, L = shards.shape
+        if not shards.flags.c_contiguous or shards.dtype != np.uint8:
+            raise ValueError("shards must be a C-contiguous uint8 array")
+        pres = np.ascontiguousarray(present, dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.cda_rs_decode(self.ctx.h, ptr(shards), ptr(pres), w // 2, L, n))
+        return shards
 
     def max_chunks(self) -> int:
         return 32768 * 32768
@@ -168,6 +194,43 @@ class ExtendedDataSquare:
 
     def data_root(self) -> bytes:
         return self._compute_roots()[2]
+
+    # -- repair -------------------------------------------------------------
+    def repair(self, row_roots, col_roots, present=None):
+        """ExtendedDataSquare.Repair(rowRoots, colRoots).
+
+        ``present`` (W, W) marks the cells that are held (rsmt2d: non-nil
+        cells); by default every cell is.  Raises ByzantineDataError (with
+        .axis / .index), UnrepairableError or CdaError("bad root input ...").
+        The square is updated in place, also on an error.
+        """
+        W = self.width()
+        if len(row_roots) != W or len(col_roots) != W:
+            raise ValueError("number of roots does not match the square width")
+        if present is None:
+            present = np.ones((W, W), dtype=np.uint8)
+        pres = np.ascontiguousarray(present, dtype=np.uint8)
+        rows = np.frombuffer(b"".join(bytes(r) for r in row_roots), dtype=np.uint8)
+        cols = np.frombuffer(b"".join(bytes(c) for c in col_roots), dtype=np.uint8)
+        ctx = getattr(self.codec, "ctx", None) or default_context()
+        if not self._eds.flags.c_contiguous:
+            self._eds = np.ascontiguousarray(self._eds)
+        axis = C.c_int32(-1)
+        index = C.c_uint32(0)
+        rc = ctx.lib.cda_repair(ctx.h, ptr(self._eds), ptr(pres), W, ptr(rows), ptr(cols), C.byref(axis),
+                                C.byref(index))
+        self._roots, self._err = None, None
+        if rc == _lib.CDA_ERR_BYZANTINE:
+            raise ByzantineDataError(rc, ctx.lib.cda_last_error(ctx.h).decode(), axis.value, index.value)
+        ctx.check(rc)
+
+
+def new_extended_data_square_with_missing(eds: np.ndarray, present: np.ndarray, codec, tree_fn):
+    """A square as a sampling node holds it: cells with present == 0 are
+    zeroed (rsmt2d nil cells)."""
+    eds = np.array(eds, dtype=np.uint8, copy=True)
+    eds[np.asarray(present) == 0] = 0
+    return ExtendedDataSquare(eds, codec, tree_fn)
 
 
 def _square_k(n: int) -> int:

@@ -423,6 +423,24 @@ int cda_square_blob_commitments(cda_square* sq, const uint32_t* starts, const ui
     });
 }
 
+int cda_repair(cda_ctx* ctx, uint8_t* eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
+               const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!eds || !present || !row_roots || !col_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
+        if (byz_axis) *byz_axis = -1;
+        return e.host_repair(eds, present, w, row_roots, col_roots, byz_axis, byz_index);
+    });
+}
+
+int cda_rs_decode(cda_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_t n_shards, uint32_t shard_len,
+                  uint32_t n_codewords) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (n_codewords == 0) return CDA_OK;
+        if (!shards || !present) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.host_rs_decode(shards, present, n_shards, shard_len, n_codewords);
+    });
+}
+
 int cda_set_profiling(cda_ctx* ctx, int enable) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
         e.set_profiling(enable != 0);

@@ -131,6 +131,11 @@ class Engine {
     int square_blob_commitments(ResidentSquare* sq, const uint32_t* starts, const uint32_t* lens, uint32_t n,
                                 uint32_t threshold, uint8_t* out);
 
+    // Repair (repair.hip): rsmt2d ExtendedDataSquare.Repair and Codec.Decode.
+    int host_repair(uint8_t* eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
+                    const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index);
+    int host_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t k, uint32_t shard_len, uint32_t n_codewords);
+
     // Stage timing with HIP events on the launch stream (bench / profiling).
     enum Stage { kStageRsQ0 = 0, kStageRsQ3, kStageOrder, kStageLeaves, kStageLevels, kStageDataRoot, kNumStages };
     void set_profiling(bool on) { profiling_ = on; }
@@ -185,6 +190,17 @@ class Engine {
     size_t sq_stage_bytes_ = 0;
     hipEvent_t sq_event_ = nullptr;
     int upload_txs(const uint8_t* txs, size_t len, hipStream_t s);
+    // repair: GF(2^8) tables (GF(2^16) ones are shared with the encoder),
+    // codeword list, error locators, presence map, parity check scratch
+    DevBuf gf8_log_, gf8_exp_, gf8_skew_, rp_cw_, rp_err_, rp_present_, rp_parity_, rp_buf_, rp_flags_;
+    std::vector<uint8_t> rp_roots_;   // roots of the last repair_verify (rows then columns)
+    int ensure_gf8_tables();
+    int repair_verify(const uint8_t* d_eds, uint32_t k, const uint8_t* row_roots, const uint8_t* col_roots,
+                      std::vector<uint8_t>& bad, hipStream_t s);
+    // Leopard decode of codewords (axis, index pairs) of a grid of 2k x 2k
+    // cells of shard_len bytes; marks them present.
+    int decode_codewords(uint8_t* d_cells, uint8_t* d_present, uint32_t k, uint32_t shard_len,
+                         const std::vector<uint32_t>& axis_index, hipStream_t s);
 };
 
 }  // namespace cda

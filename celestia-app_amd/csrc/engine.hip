@@ -48,7 +48,8 @@ Engine::~Engine() {
     for (DevBuf* b : {&gf16_chunk_[0], &gf16_chunk_[1], &gf16_log_, &gf16_exp_,
                       &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &h_ods_, &h_eds_,
                       &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_, &cm_plan_, &cm_tables_,
-                      &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_})
+                      &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_, &gf8_log_, &gf8_exp_, &gf8_skew_, &rp_cw_,
+                      &rp_err_, &rp_present_, &rp_parity_, &rp_buf_, &rp_flags_})
         b->release();
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);

@@ -28,6 +28,8 @@
  *                          app/prepare_proposal.go:50, app/extend_block.go:16)
  *   cda_blob_commitments   go-square inclusion.CreateCommitment
  *                          (x/blob/types/blob_tx.go:98, payforblob.go:53)
+ *   cda_repair             rsmt2d ExtendedDataSquare.Repair (EXT v0.14.0)
+ *   cda_rs_decode          rsmt2d Codec.Decode (reedsolomon Reconstruct)
  *   cda_square_*           resident squares: proof.NewShareInclusionProofFromEDS
  *                          (pkg/proof/proof.go:77), inclusion.GetCommitment
  *                          (pkg/inclusion/get_commit.go:12)
@@ -70,7 +72,10 @@ enum {
     CDA_ERR_OOM = -5,           /* device allocation failure */
     CDA_ERR_INVALID = -6,       /* bad argument (NULL pointer, k out of range, ...) */
     CDA_ERR_UNSUPPORTED = -7,   /* shard count the codec does not support */
-    CDA_ERR_SQUARE = -8         /* go-square square.Construct / Build error (message from cda_last_error) */
+    CDA_ERR_SQUARE = -8,        /* go-square square.Construct / Build error (message from cda_last_error) */
+    CDA_ERR_BYZANTINE = -9,     /* rsmt2d ErrByzantineData ("byzantine row: %d" / "byzantine col: %d") */
+    CDA_ERR_UNREPAIRABLE = -10  /* rsmt2d ErrUnrepairableDataSquare ("failed to solve data square") /
+                                   reedsolomon ErrTooFewShards */
 };
 
 typedef struct cda_ctx cda_ctx;
@@ -258,6 +263,23 @@ int cda_square_share_proof(cda_square *sq, uint32_t start, uint32_t end, uint8_t
  * reference does) and spans share_lens[i] shares; commitments n*32. */
 int cda_square_blob_commitments(cda_square *sq, const uint32_t *starts, const uint32_t *share_lens, uint32_t n,
                                 uint32_t threshold, uint8_t *commitments);
+
+/* ---- Repair ------------------------------------------
+ * rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots) (EXT v0.14.0,
+ * go.mod:13; used by light / full nodes after sampling).  eds: w*w*512 bytes,
+ * in/out; present: w*w bytes (0 = missing: the cell's bytes are ignored and
+ * reconstructed).  row_roots / col_roots: w*90 bytes each (the DAH).
+ * Returns CDA_OK (eds complete), CDA_ERR_BYZANTINE (*byz_axis 0 row / 1 col,
+ * *byz_index), CDA_ERR_UNREPAIRABLE, or CDA_ERR_INVALID for a complete vector
+ * whose root differs from the given one ("bad root input: ..."). */
+int cda_repair(cda_ctx *ctx, uint8_t *eds, const uint8_t *present, uint32_t w, const uint8_t *row_roots,
+               const uint8_t *col_roots, int32_t *byz_axis, uint32_t *byz_index);
+/* rsmt2d Codec.Decode (LeoRSCodec -> reedsolomon Reconstruct): n_codewords
+ * codewords of 2*n_shards shards of shard_len bytes (multiple of 64),
+ * contiguous; shards with present[] == 0 are reconstructed in place (data
+ * and parity).  Fewer than n_shards present: CDA_ERR_UNREPAIRABLE. */
+int cda_rs_decode(cda_ctx *ctx, uint8_t *shards, const uint8_t *present, uint32_t n_shards, uint32_t shard_len,
+                  uint32_t n_codewords);
 
 /* Stage timing (HIP events on the launch stream).  When enabled, every
  * enqueued stage is bracketed by events; cda_stage_times synchronises them and
