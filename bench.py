@@ -222,6 +222,79 @@ def square_construction(ctx, dev, stream, max_ss: int = 128, reps: int = 20) -> 
             "data_root": d_root.cpu().numpy().tobytes().hex()}
 
 
+def eds_repair(ctx, k: int = 128, reps: int = 5) -> dict:
+    """rsmt2d ExtendedDataSquare.Repair on the GPU
+    (cda_repair, host buffers in/out, so PCIe is inside the figure) for two
+    erasure patterns of one random k=128 square: the whole original quadrant
+    lost (one sweep: every row decodes from its parity half), and a random
+    half of every row lost (rows alone cannot all finish; columns complete
+    them).  Each repaired square is checked against the extension."""
+    import ctypes as C
+
+    import numpy as np
+
+    from celestia_da import da, testfactory
+    from celestia_da._lib import ptr
+
+    W = 2 * k
+    ods = testfactory.random_square(k, 7)
+    sq = da.extend_shares(ods)
+    dah = da.new_data_availability_header(sq)
+    full = np.ascontiguousarray(sq.array())
+    rows = np.frombuffer(b"".join(dah.row_roots), dtype=np.uint8)
+    cols = np.frombuffer(b"".join(dah.column_roots), dtype=np.uint8)
+    rng = np.random.default_rng(5)
+    pats = {"q0_lost": np.ones((W, W), np.uint8), "half_of_every_row_lost": np.ones((W, W), np.uint8)}
+    pats["q0_lost"][:k, :k] = 0
+    for r in range(W):
+        pats["half_of_every_row_lost"][r, rng.choice(W, k, replace=False)] = 0
+    out = {"k": k, "buffers": "host (PCIe inside the timing)"}
+    for name, p in pats.items():
+        times = []
+        for _ in range(reps + 1):
+            e = np.where(p[..., None].astype(bool), full, 0).astype(np.uint8)
+            ax, ix = C.c_int32(-1), C.c_uint32(0)
+            a = time.perf_counter()
+            rc = ctx.lib.cda_repair(ctx.h, ptr(e), ptr(p), W, ptr(rows), ptr(cols), C.byref(ax), C.byref(ix))
+            times.append(time.perf_counter() - a)
+            ctx.check(rc)
+            assert np.array_equal(e, full), "repaired square differs"
+        ms = 1e3 * sorted(times[1:])[len(times[1:]) // 2]
+        out[name] = {"erased_cells": int((p == 0).sum()), "ms": ms}
+    return out
+
+
+def share_proofs(ctx, k: int = 128, reps: int = 200) -> dict:
+    """proof.NewShareInclusionProofFromEDS served from a
+    resident square (cda_square_create keeps the EDS, every row-tree level and
+    the data-root tree in HBM; each proof is index arithmetic + one gather).
+    Reports the create time and the median wall time of one proof for a
+    one-share range and a 2-row range (host output buffers)."""
+    import numpy as np
+
+    from celestia_da import proof as gpr
+    from celestia_da import testfactory
+
+    ods = testfactory.random_square(k, 11)
+    a = time.perf_counter()
+    sq = gpr.ResidentSquare(ods)
+    create_ms = 1e3 * (time.perf_counter() - a)
+    out = {"k": k, "create_ms_wall": create_ms}
+    try:
+        for name, (s, e) in {"one_share": (5 * k + 3, 5 * k + 4), "two_rows": (7 * k + 10, 9 * k - 10)}.items():
+            ns = bytes(np.asarray(ods[s])[:29])
+            sq.share_proof(ns, s, e)
+            t = []
+            for _ in range(reps):
+                b = time.perf_counter()
+                sq.share_proof(ns, s, e)
+                t.append(time.perf_counter() - b)
+            out[name] = {"shares": e - s, "us_wall": 1e6 * sorted(t)[len(t) // 2]}
+    finally:
+        sq.close()
+    return out
+
+
 def blob_commitments(ctx, dev, stream, n_blocks: int = 64, reps: int = 10) -> dict:
     """inclusion.CreateCommitment for every blob of
     n_blocks full k=128 blocks (blobfactory.full_block_blobs), blob bytes
@@ -396,6 +469,14 @@ def main():
             extras["blob_commitments"] = blob_commitments(ctx, dev, stream)
         except Exception as e:
             extras["blob_commitments"] = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            extras["share_proofs"] = share_proofs(ctx)
+        except Exception as e:
+            extras["share_proofs"] = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            extras["eds_repair"] = eds_repair(ctx)
+        except Exception as e:
+            extras["eds_repair"] = {"error": f"{type(e).__name__}: {e}"}
         # config 3: one 512 x 512 square (GF(2^16), 512 MiB EDS)
         del d_eds
         torch.cuda.empty_cache()

@@ -82,7 +82,14 @@ int Engine::init() {
     int rc;
     if ((rc = check(hipSetDevice(device_), "hipSetDevice"))) return rc;
     if ((rc = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
-    if ((rc = check(hipStreamCreateWithFlags(&rs_stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
+    // lower value is a higher priority), so RS workgroups win free CU slots.
+    if (const char* env = getenv("CDA_RS_PRIORITY")) {
+        if ((rc = check(hipStreamCreateWithPriority(&rs_stream_, hipStreamNonBlocking, atoi(env)), "hipStreamCreate")))
+            return rc;
+    } else if ((rc = check(hipStreamCreateWithFlags(&rs_stream_, hipStreamNonBlocking), "hipStreamCreate"))) {
+        return rc;
+    }
     if ((rc = check(hipStreamCreateWithFlags(&hash_stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.

@@ -29,9 +29,18 @@ namespace {
 
 using namespace bs8;
 
+// Tuning knob: CDA_RS8_NUM_VGPR caps the kernel's VGPRs (the attribute counts
+// half of gfx950's unified file) so that a leaf-kernel wave fits beside the
+// two RS waves of a SIMD when the two-stream pipeline co-runs them.
+#ifdef CDA_RS8_NUM_VGPR
+#define CDA_RS8_ATTR __attribute__((amdgpu_num_vgpr(CDA_RS8_NUM_VGPR)))
+#else
+#define CDA_RS8_ATTR
+#endif
+
 constexpr uint32_t kLdsBytes = 8 * 8 * 8 * 64 * 4;   // E[u][tt][p][lane] dwords
 
-__global__ __launch_bounds__(512) void rs8_bs_kernel(const RsJob job) {
+__global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob job) {
     extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = threadIdx.x & 63;
