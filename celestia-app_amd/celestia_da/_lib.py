@@ -44,7 +44,7 @@ EXPORTED = (
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
     "cda_blob_commitments", "cda_blob_commitments_device",
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
-    "cda_square_blob_commitments", "cda_repair", "cda_rs_decode",
+    "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -137,6 +137,7 @@ def load():
                                              u8p, u8p, u8p]
         L.cda_square_blob_commitments.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint32, u8p]
         L.cda_repair.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
+        L.cda_repair_device.argtypes = [ctxp, vp, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
         L.cda_rs_decode.argtypes = [ctxp, u8p, u8p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]

@@ -432,6 +432,15 @@ int cda_repair(cda_ctx* ctx, uint8_t* eds, const uint8_t* present, uint32_t w, c
     });
 }
 
+int cda_repair_device(cda_ctx* ctx, void* d_eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
+                      const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!d_eds || !present || !row_roots || !col_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
+        if (byz_axis) *byz_axis = -1;
+        return e.device_repair(static_cast<uint8_t*>(d_eds), present, w, row_roots, col_roots, byz_axis, byz_index);
+    });
+}
+
 int cda_rs_decode(cda_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_t n_shards, uint32_t shard_len,
                   uint32_t n_codewords) {
     return guarded(ctx, [&](cda::Engine& e) -> int {

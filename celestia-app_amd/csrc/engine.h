@@ -134,6 +134,10 @@ class Engine {
     // Repair (repair.hip): rsmt2d ExtendedDataSquare.Repair and Codec.Decode.
     int host_repair(uint8_t* eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
                     const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index);
+    int device_repair(uint8_t* d_eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
+                      const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index);
+    int repair(uint8_t* eds, uint8_t* d_eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
+               const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index);
     int host_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t k, uint32_t shard_len, uint32_t n_codewords);
 
     // Stage timing with HIP events on the launch stream (bench / profiling).

@@ -312,8 +312,8 @@ int Engine::repair_verify(const uint8_t* E, uint32_t k, const uint8_t* row_roots
     return CDA_OK;
 }
 
-// rsmt2d ExtendedDataSquare.Repair on a host EDS (cells whose present[] is 0
-// are ignored and overwritten).  Returns CDA_OK, CDA_ERR_BYZANTINE (axis /
+// rsmt2d ExtendedDataSquare.Repair on a host or device EDS (cells whose
+// present[] is 0 are ignored and overwritten).  Returns CDA_OK, CDA_ERR_BYZANTINE (axis /
 // index in *byz_axis / *byz_index), CDA_ERR_UNREPAIRABLE or CDA_ERR_INVALID
 // ("bad root input").  The square is copied back in every one of these
 // outcomes (partially repaired on an error).
@@ -330,24 +330,48 @@ int Engine::repair_verify(const uint8_t* E, uint32_t k, const uint8_t* row_roots
 // names the same first byzantine vector as rsmt2d.
 int Engine::host_repair(uint8_t* eds, const uint8_t* present_in, uint32_t W, const uint8_t* row_roots,
                         const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index) {
+    return repair(eds, nullptr, present_in, W, row_roots, col_roots, byz_axis, byz_index);
+}
+
+int Engine::device_repair(uint8_t* d_eds, const uint8_t* present_in, uint32_t W, const uint8_t* row_roots,
+                          const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index) {
+    // the square may have been written on any stream of the caller
+    if (int rc = check(hipDeviceSynchronize(), "hipDeviceSynchronize")) return rc;
+    return repair(nullptr, d_eds, present_in, W, row_roots, col_roots, byz_axis, byz_index);
+}
+
+// One of `eds` (host) / `d_eds` (device, repaired in place) is set.  The
+// host square is staged in h_eds_; a device square keeps a pristine copy in
+// rp_buf_ for the exact replay.
+int Engine::repair(uint8_t* eds, uint8_t* d_eds, const uint8_t* present_in, uint32_t W, const uint8_t* row_roots,
+                   const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index) {
     const uint32_t k = W / 2;
     if (W < 2 || (W & (W - 1)) || k > 512) return fail(CDA_ERR_INVALID, "EDS width must be a power of two in [2, 1024]");
     const size_t eds_b = (size_t)W * W * kShare, roots_b = (size_t)W * kNode;
     hipStream_t s = stream_;
     int rc;
-    if ((rc = check(h_eds_.ensure(eds_b), "hipMalloc"))) return rc;
+    DevBuf& stage = d_eds ? rp_buf_ : h_eds_;
+    if ((rc = check(stage.ensure(eds_b), "hipMalloc"))) return rc;
     if ((rc = check(rp_present_.ensure((size_t)W * W), "hipMalloc"))) return rc;
     if ((rc = check(h_rows_.ensure(roots_b), "hipMalloc"))) return rc;
     if ((rc = check(h_cols_.ensure(roots_b), "hipMalloc"))) return rc;
     if ((rc = check(h_roots_.ensure(32), "hipMalloc"))) return rc;
     if ((rc = check(err_buf_.ensure(4), "hipMalloc"))) return rc;
     std::vector<uint8_t> present;
-    uint8_t* E = h_eds_.as<uint8_t>();
+    uint8_t* E = d_eds ? d_eds : h_eds_.as<uint8_t>();
+    bool first = true;
     auto upload = [&]() -> int {
         present.assign(present_in, present_in + (size_t)W * W);
         for (auto& v : present) v = v ? 1 : 0;
         int r;
-        if ((r = check(hipMemcpyAsync(E, eds, eds_b, hipMemcpyHostToDevice, s), "H2D"))) return r;
+        if (!d_eds) {
+            if ((r = check(hipMemcpyAsync(E, eds, eds_b, hipMemcpyHostToDevice, s), "H2D"))) return r;
+        } else if (first) {
+            if ((r = check(hipMemcpyAsync(stage.ptr, E, eds_b, hipMemcpyDeviceToDevice, s), "D2D"))) return r;
+        } else if ((r = check(hipMemcpyAsync(E, stage.ptr, eds_b, hipMemcpyDeviceToDevice, s), "D2D"))) {
+            return r;
+        }
+        first = false;
         if ((r = check(hipMemcpyAsync(rp_present_.ptr, present.data(), present.size(), hipMemcpyHostToDevice, s),
                        "H2D")))
             return r;
@@ -363,7 +387,7 @@ int Engine::host_repair(uint8_t* eds, const uint8_t* present_in, uint32_t W, con
     };
     auto download = [&](int code) -> int {
         int r;
-        if ((r = check(hipMemcpyAsync(eds, E, eds_b, hipMemcpyDeviceToHost, s), "D2H"))) return r;
+        if (!d_eds && (r = check(hipMemcpyAsync(eds, E, eds_b, hipMemcpyDeviceToHost, s), "D2H"))) return r;
         if ((r = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return r;
         return code;
     };

@@ -274,6 +274,12 @@ int cda_square_blob_commitments(cda_square *sq, const uint32_t *starts, const ui
  * whose root differs from the given one ("bad root input: ..."). */
 int cda_repair(cda_ctx *ctx, uint8_t *eds, const uint8_t *present, uint32_t w, const uint8_t *row_roots,
                const uint8_t *col_roots, int32_t *byz_axis, uint32_t *byz_index);
+/* cda_repair on an HBM-resident square (d_eds: w*w*512 device bytes, repaired
+ * in place; present and the roots stay host buffers).  Same outcomes and
+ * messages; the work is ordered after everything already queued on the
+ * device and complete when the call returns. */
+int cda_repair_device(cda_ctx *ctx, void *d_eds, const uint8_t *present, uint32_t w, const uint8_t *row_roots,
+                      const uint8_t *col_roots, int32_t *byz_axis, uint32_t *byz_index);
 /* rsmt2d Codec.Decode (LeoRSCodec -> reedsolomon Reconstruct): n_codewords
  * codewords of 2*n_shards shards of shard_len bytes (multiple of 64),
  * contiguous; shards with present[] == 0 are reconstructed in place (data

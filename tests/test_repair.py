@@ -254,3 +254,60 @@ def test_repair_k512_round_trip(ctx):
     assert out == "ok"
     assert np.array_equal(rep[:k, :k].reshape(-1, 512), ods)
     assert np.array_equal(rep, sq.array())
+
+
+def device_repair(ctx, eds, present, rows, cols):
+    """cda_repair_device on an HBM-resident copy of the square."""
+    import ctypes as C
+
+    import torch
+
+    from celestia_da._lib import ptr
+    W = eds.shape[0]
+    e = np.where(np.asarray(present, bool)[..., None], eds, 0).astype(np.uint8)
+    d = torch.from_numpy(e.reshape(-1)).to("cuda")
+    p = np.ascontiguousarray(present, dtype=np.uint8)
+    rb = np.frombuffer(b"".join(bytes(r) for r in rows), dtype=np.uint8)
+    cb = np.frombuffer(b"".join(bytes(c) for c in cols), dtype=np.uint8)
+    ax, ix = C.c_int32(-1), C.c_uint32(0)
+    rc = ctx.lib.cda_repair_device(ctx.h, d.data_ptr(), ptr(p), W, ptr(rb), ptr(cb), C.byref(ax), C.byref(ix))
+    out = d.cpu().numpy().reshape(W, W, 512)
+    if rc == 0:
+        return "ok", out
+    if rc == -9:
+        return ("byz", ax.value, ix.value), None
+    if rc == -10:
+        return "unrep", None
+    assert rc == -6 and "bad root input" in ctx.lib.cda_last_error(ctx.h).decode()
+    return "badroot", None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [4, 16, 128])
+def test_repair_device_matches_host(ctx, k):
+    """The HBM-resident entry point gives the host entry point's outcome and
+    square for ordinary, byzantine, unrepairable and bad-root inputs."""
+    eds, rows, cols = small_eds(k, 12)
+    W = 2 * k
+    rng = np.random.default_rng(3000 + k)
+    cases = []
+    for trial in range(3):
+        cases.append((eds, rng.random((W, W)) < (0.4 + 0.15 * trial)))
+    q0 = np.ones((W, W), bool)
+    q0[:k, :k] = False
+    cases.append((eds, q0))
+    bad = eds.copy()
+    bad[1, 2, 77] ^= 0x40
+    cases.append((bad, np.ones((W, W), bool)))                # bad root input
+    p = np.ones((W, W), bool)
+    p[0, 1] = False
+    cases.append((bad, p))                                    # decode exposes the corruption
+    none = np.zeros((W, W), bool)
+    none[: max(1, k - 1), :] = True
+    cases.append((eds, none))                                 # unrepairable
+    for i, (sq, p) in enumerate(cases):
+        h = gpu_repair(ctx, sq, p, rows, cols)
+        d = device_repair(ctx, sq, p, rows, cols)
+        assert h[0] == d[0], (i, h[0], d[0])
+        if h[0] == "ok":
+            assert np.array_equal(h[1], d[1]) and np.array_equal(d[1], eds)
