@@ -244,12 +244,14 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     const uint64_t off[2] = {0, slots_sq / 2};
     if ((rc = run_forests(f, 2, W, n, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), slots_sq, off, s))) return rc;
     mark_end(s);
-    mark_begin(kStageDataRoot, s);
-    if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
-    if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s),
-                    "data root")))
-        return rc;
-    mark_end(s);
+    if (d_roots) {   // NULL: roots only (repair verification needs no data root)
+        mark_begin(kStageDataRoot, s);
+        if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
+        if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s),
+                        "data root")))
+            return rc;
+        mark_end(s);
+    }
     if (d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
     return CDA_OK;
 }

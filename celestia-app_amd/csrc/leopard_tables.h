@@ -75,6 +75,24 @@ constexpr LeoField<8> make_gf8() {
     return F;
 }
 
+// 2-bit-chunk multiply tables for GF(2^8): for the constant with log L,
+// c[q] byte e = mul_log(e << 2q, L), so v_perm_b32(c[q], c[q], (y >> 2q) &
+// 0x03030303) multiplies chunk q of four packed symbols; the four partial
+// products XOR to L * y.  L = 255 (the modulus) is the identity.
+struct Mul8Chunks {
+    uint32_t c[4];
+};
+struct Mul8All {
+    Mul8Chunks t[256];
+};
+constexpr Mul8All make_all_mul8(const LeoField<8>& F) {
+    Mul8All a{};
+    for (uint32_t l = 0; l < 256; l++)
+        for (uint32_t q = 0; q < 4; q++)
+            for (uint32_t e = 0; e < 4; e++) a.t[l].c[q] |= (uint32_t)F.mul_log(e << (2 * q), l) << (8 * e);
+    return a;
+}
+
 // ---------------------------------------------------------------------------
 // v_perm_b32 nibble lookup.  For a 16-entry byte table T and nibble vector n
 // (four byte lanes, each 0..15):

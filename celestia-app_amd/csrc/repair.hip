@@ -168,6 +168,100 @@ __global__ __launch_bounds__(256) void decode_kernel(FieldDev F, const Cw* __res
     }
 }
 
+// GF(2^8) decode, dword form: a thread handles 4 packed symbols (one dword of
+// a shard's 64-B column block) per step, and multiplies by a runtime constant
+// with the 2-bit-chunk v_perm tables of all 255 logs (make_all_mul8), staged
+// in LDS with the skew vector: 4 v_perm + 7 selector ops per 4 symbols instead
+// of two dependent log/exp lookups per symbol.  Same algorithm and order as
+// decode_kernel<8>.
+constexpr Mul8All kMul8Dec = make_all_mul8(make_gf8());
+__constant__ Mul8All kMul8Tab = kMul8Dec;
+
+__device__ __forceinline__ uint32_t mul8v(uint32_t y, const uint4 T) {
+    const uint32_t m = 0x03030303u;
+    const uint32_t p0 = __builtin_amdgcn_perm(T.x, T.x, y & m);
+    const uint32_t p1 = __builtin_amdgcn_perm(T.y, T.y, (y >> 2) & m);
+    const uint32_t p2 = __builtin_amdgcn_perm(T.z, T.z, (y >> 4) & m);
+    const uint32_t p3 = __builtin_amdgcn_perm(T.w, T.w, (y >> 6) & m);
+    return p0 ^ p1 ^ p2 ^ p3;
+}
+
+__global__ __launch_bounds__(256) void decode8_kernel(const uint16_t* __restrict__ skew, const Cw* __restrict__ cws,
+                                                      uint8_t* __restrict__ eds, const uint8_t* __restrict__ present,
+                                                      uint32_t k, const uint16_t* __restrict__ errloc,
+                                                      uint32_t shard_len) {
+    constexpr uint32_t Q = 16;   // dwords per 64-B column block
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds8[];   // tab[256] uint4 | skew[256] u16 | work | tmp
+    uint4* tab = reinterpret_cast<uint4*>(lds8);
+    uint16_t* sk = reinterpret_cast<uint16_t*>(lds8 + 1024);
+    const uint32_t n = 2 * k, W = 2 * k, tid = threadIdx.x, nt = blockDim.x;
+    uint32_t* work = lds8 + 1024 + 128;
+    uint32_t* tmp = work + n * Q;
+    const uint32_t blocks = shard_len / 64;
+    const uint32_t cwi = blockIdx.x / blocks, blk = blockIdx.x % blocks;
+    const Cw c = cws[cwi];
+    const uint16_t* el = errloc + (size_t)cwi * n;
+    for (uint32_t i = tid; i < 256; i += nt) {
+        const Mul8Chunks& t = kMul8Tab.t[i];
+        tab[i] = make_uint4(t.c[0], t.c[1], t.c[2], t.c[3]);
+        sk[i] = i < 255 ? skew[i] : 255;
+    }
+    __syncthreads();
+    for (uint32_t it = tid; it < n * Q; it += nt) {
+        const uint32_t p = it / Q, q = it % Q, w = p ^ k;
+        const uint32_t off = cell_off(c, p, W);
+        uint32_t x = 0;
+        if (present[off]) {
+            x = *reinterpret_cast<const uint32_t*>(eds + (size_t)off * shard_len + blk * 64 + 4 * q);
+            x = mul8v(x, tab[el[w]]);
+        }
+        work[w * Q + q] = x;
+    }
+    __syncthreads();
+    for (uint32_t d = 1; d < n; d <<= 1) {   // IFFT (ifftDITDecoder, skew offset 0)
+        for (uint32_t it = tid; it < (n / 2) * Q; it += nt) {
+            const uint32_t b = it / Q, q = it % Q;
+            const uint32_t g = (b / d) * 2 * d, i = g + (b % d);
+            const uint32_t L = sk[g + d - 1];
+            uint32_t x = work[i * Q + q], y = work[(i + d) * Q + q];
+            y ^= x;
+            if (L != 255) x ^= mul8v(y, tab[L]);
+            work[i * Q + q] = x;
+            work[(i + d) * Q + q] = y;
+        }
+        __syncthreads();
+    }
+    for (uint32_t it = tid; it < n * Q; it += nt) {   // formal derivative (see decode_kernel)
+        const uint32_t p = it / Q, q = it % Q;
+        uint32_t x = work[p * Q + q];
+        for (uint32_t w = 1; w < n; w <<= 1)
+            if (((p / w) & 1) == 0 && (p / w + 1) * w < n) x ^= work[(p + w) * Q + q];
+        tmp[p * Q + q] = x;
+    }
+    __syncthreads();
+    for (uint32_t d = n / 2; d >= 1; d >>= 1) {   // FFT (fftDIT, skew offset 0)
+        for (uint32_t it = tid; it < (n / 2) * Q; it += nt) {
+            const uint32_t b = it / Q, q = it % Q;
+            const uint32_t g = (b / d) * 2 * d, i = g + (b % d);
+            const uint32_t L = sk[g + d - 1];
+            uint32_t x = tmp[i * Q + q], y = tmp[(i + d) * Q + q];
+            if (L != 255) x ^= mul8v(y, tab[L]);
+            y ^= x;
+            tmp[i * Q + q] = x;
+            tmp[(i + d) * Q + q] = y;
+        }
+        __syncthreads();
+    }
+    for (uint32_t it = tid; it < n * Q; it += nt) {   // reveal erasures: work * g^(255 - errLoc)
+        const uint32_t p = it / Q, q = it % Q;
+        const uint32_t off = cell_off(c, p, W);
+        if (present[off]) continue;
+        const uint32_t w = p ^ k;
+        *reinterpret_cast<uint32_t*>(eds + (size_t)off * shard_len + blk * 64 + 4 * q) =
+            mul8v(tmp[w * Q + q], tab[255 - el[w]]);
+    }
+}
+
 // Mark every cell of the listed codewords present.
 __global__ void mark_kernel(const Cw* __restrict__ cws, uint32_t n_cw, uint8_t* __restrict__ present, uint32_t W) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
@@ -233,7 +327,8 @@ int Engine::decode_codewords(uint8_t* d_eds, uint8_t* d_present, uint32_t k, uin
     const uint32_t S = k <= 128 ? 64 : 32;
     const size_t lds = (size_t)2 * n * S * 2;
     if (k <= 128) {
-        hipLaunchKernelGGL(decode_kernel<8>, dim3(n_cw * (shard_len / 64)), dim3(256), lds, s, F, rp_cw_.as<Cw>(),
+        const size_t lds8 = (1024 + 128 + (size_t)2 * n * 16) * 4;
+        hipLaunchKernelGGL(decode8_kernel, dim3(n_cw * (shard_len / 64)), dim3(256), lds8, s, F.skew, rp_cw_.as<Cw>(),
                            d_eds, d_present, k, rp_err_.as<uint16_t>(), shard_len);
     } else {
         if (lds > 64 * 1024 &&
@@ -278,8 +373,8 @@ int Engine::repair_verify(const uint8_t* E, uint32_t k, const uint8_t* row_roots
     int rc;
     if ((rc = check(rp_parity_.ensure((size_t)2 * W * k * SH), "hipMalloc"))) return rc;
     if ((rc = check(rp_flags_.ensure((size_t)2 * W * 4), "hipMalloc"))) return rc;
-    if ((rc = enqueue_dah(E, k, 1, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(), h_roots_.as<uint8_t>(),
-                          err_buf_.as<uint32_t>(), nullptr, s)))
+    if ((rc = enqueue_dah(E, k, 1, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(), nullptr, err_buf_.as<uint32_t>(),
+                          nullptr, s)))
         return rc;
     RsJob j{};
     j.src = E;

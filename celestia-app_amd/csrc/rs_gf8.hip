@@ -29,23 +29,10 @@ namespace {
 
 constexpr LeoField<8> kF8 = make_gf8();
 
-// 2-bit-chunk tables: c[q] byte e = mul_log(e << 2q, L).  v_perm_b32(T, T, sel)
+// 2-bit-chunk tables (leopard_tables.h make_all_mul8).  v_perm_b32(T, T, sel)
 // with sel bytes in 0..3 reads byte sel of T and needs one SGPR operand, so the
 // four table dwords are scalar immediates (s_mov) -- no VGPR materialisation.
-struct Mul8Chunks {
-    uint32_t c[4];
-};
-struct Mul8All {
-    Mul8Chunks t[256];
-};
-constexpr Mul8All make_all_mul8() {
-    Mul8All a{};
-    for (uint32_t l = 0; l < 256; l++)
-        for (uint32_t q = 0; q < 4; q++)
-            for (uint32_t e = 0; e < 4; e++) a.t[l].c[q] |= (uint32_t)kF8.mul_log(e << (2 * q), l) << (8 * e);
-    return a;
-}
-constexpr Mul8All kMul8 = make_all_mul8();
+constexpr Mul8All kMul8 = make_all_mul8(kF8);
 constexpr uint16_t kMod8 = 255;
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
