@@ -429,11 +429,12 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    assert int(d_status.abs().sum().item()) == 0, "push-order status set on ordered input"
-    # tiled inputs must give tiled data roots
-    roots = d_roots.view(B, 32).cpu().numpy()
-    for i in range(nd, B):
-        assert (roots[i] == roots[i % nd]).all()
+    if not os.environ.get("CDA_BENCH_NOCHECK"):   # set only for timing-diagnostic library variants
+        assert int(d_status.abs().sum().item()) == 0, "push-order status set on ordered input"
+        # tiled inputs must give tiled data roots
+        roots = d_roots.view(B, 32).cpu().numpy()
+        for i in range(nd, B):
+            assert (roots[i] == roots[i % nd]).all()
 
     ctx.set_profiling(True)
     ctx.stage_times()

@@ -123,23 +123,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEAF_WA
     uint32_t nxt[16];
     load_raw16(src + 4, nxt);
 #endif
-    // block 0: 0x00 || ns(29) || share[0:34]
-    if (parity) {
-        w[0] = 0x00FFFFFFu;
+    // block 0: 0x00 || ns(29) || share[0:34]; a parity leaf's first 7 words
+    // are constant, so it starts from the precomputed mid-state
 #pragma unroll
-        for (int i = 1; i < 7; i++) w[i] = 0xFFFFFFFFu;
+    for (int i = 8; i < 16; i++) w[i] = body_word(cur[i - 8], cur[i - 7]);
+    if (parity) {
         w[7] = __builtin_amdgcn_perm(cur[0], cur[0], 0x0D0D0001u);
+        sha_compress_from<kLeafParityRounds>(st, kLeafParityMid, kLeafParityHead, w);
     } else {
         w[0] = __builtin_amdgcn_perm(cur[0], cur[0], 0x0C000102u);
 #pragma unroll
         for (int i = 1; i < 7; i++) w[i] = __builtin_amdgcn_perm(cur[i], cur[i - 1], 0x03040506u);
         w[7] = __builtin_amdgcn_perm(cur[7], cur[6], 0x03040C0Cu) | __builtin_amdgcn_perm(cur[0], cur[0], 0x0C0C0001u);
+        sha_compress(st, w);
     }
 #pragma unroll
-    for (int i = 8; i < 16; i++) w[i] = body_word(cur[i - 8], cur[i - 7]);
-#pragma unroll
     for (int i = 0; i < 8; i++) tail[i] = cur[8 + i];
-    sha_compress(st, w);
 
 #pragma unroll 1
     for (int b = 1; b < 8; b++) {
@@ -215,7 +214,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
     const size_t sq = blockIdx.y;
     uint32_t t, p;
     if (F.node_stride == 1) {
-        t = idx / n_out; p = idx % n_out;
+        // all trees' left-half parents first, then the right halves: a wave
+        // then never mixes parents with a data and a parity left child (the
+        // mid-state branch below stays uniform); runs of n_out/2 parents of
+        // one tree remain adjacent, so slot loads stay coalesced
+        if (n_out >= 2) {
+            const uint32_t hn = n_out / 2, per = F.n_trees * hn;
+            const uint32_t h = idx / per, r = idx % per;
+            t = r / hn; p = h * hn + r % hn;
+        } else {
+            t = idx; p = 0;
+        }
     } else {
         p = idx / F.n_trees; t = idx % F.n_trees;
     }
@@ -227,8 +236,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
     load_slot_be(rr, R);
     ShaState st;
     sha_init(st);
+    // block 0 = 0x01 || L[0:63]: a parity left child makes words 0..13 constant
+    if (is_parity_min(L)) {
+        w[14] = node_msg(L, R, 14);
+        w[15] = node_msg(L, R, 15);
+        sha_compress_from<kNodeParityRounds>(st, kNodeParityMid, kNodeParityHead, w);
+    } else {
 #pragma unroll
-    for (int b = 0; b < 3; b++) {
+        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, i);
+        sha_compress(st, w);
+    }
+#pragma unroll
+    for (int b = 1; b < 3; b++) {
 #pragma unroll
         for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
         sha_compress(st, w);

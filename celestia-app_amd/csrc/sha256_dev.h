@@ -92,6 +92,85 @@ CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
 
 
 // ---------------------------------------------------------------------------
+// Constant message prefixes.  Two hot messages start with constant words:
+//   parity leaf, block 0:   0x00 || 0xFF*29 || share...   -> words 0..6
+//   inner node whose left child is a parity subtree (min = max = 0xFF*29),
+//   block 0:                0x01 || 0xFF*58 || hash...     -> words 0..13
+// (3/4 of all leaves and of all inner nodes of an EDS).  The working state
+// after those rounds is a compile-time constant (sha_mid), so the
+// compression restarts at round R0 (sha_compress_from); schedule words that
+// only involve the constant words fold at compile time.
+// ---------------------------------------------------------------------------
+struct ShaMid {
+    uint32_t v[8];   // a..h after R0 rounds from the initial hash value
+};
+constexpr uint32_t crotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+template <int R0>
+constexpr ShaMid sha_mid(const uint32_t (&w)[16]) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    uint32_t a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
+    uint32_t e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+    for (int i = 0; i < R0; i++) {
+        const uint32_t S1 = crotr(e, 6) ^ crotr(e, 11) ^ crotr(e, 25);
+        const uint32_t t1 = h + S1 + ((e & f) ^ (~e & g)) + K[i] + w[i];
+        const uint32_t S0 = crotr(a, 2) ^ crotr(a, 13) ^ crotr(a, 22);
+        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    return ShaMid{{a, b, c, d, e, f, g, h}};
+}
+constexpr uint32_t kLeafParityHead[16] = {0x00FFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                          0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+constexpr uint32_t kNodeParityHead[16] = {0x01FFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                          0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                          0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+constexpr int kLeafParityRounds = 7;
+constexpr int kNodeParityRounds = 14;
+inline constexpr ShaMid kLeafParityMid = sha_mid<kLeafParityRounds>(kLeafParityHead);
+inline constexpr ShaMid kNodeParityMid = sha_mid<kNodeParityRounds>(kNodeParityHead);
+
+// First compression of a message whose words 0..R0-1 are HEAD (s holds the
+// initial hash value); w[R0..15] are the variable words.  Schedule terms of
+// constant words are computed with plain operators so they fold.
+template <int R0>
+CDA_HD void sha_compress_from(ShaState& s, const ShaMid& m, const uint32_t (&head)[16], uint32_t w[16]) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+#pragma unroll
+    for (int i = 0; i < R0; i++) w[i] = head[i];
+    uint32_t a = m.v[0], b = m.v[1], c = m.v[2], d = m.v[3];
+    uint32_t e = m.v[4], f = m.v[5], g = m.v[6], h = m.v[7];
+    bool kc[16];   // w[j] known at compile time
+#pragma unroll
+    for (int j = 0; j < 16; j++) kc[j] = j < R0;
+#pragma unroll
+    for (int i = R0; i < 64; i++) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            const int j15 = (i - 15) & 15, j2 = (i - 2) & 15, j16 = i & 15, j7 = (i - 7) & 15;
+            const uint32_t w15 = w[j15], w2 = w[j2];
+            const uint32_t s0 = kc[j15] ? (crotr(w15, 7) ^ crotr(w15, 18) ^ (w15 >> 3))
+                                        : xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = kc[j2] ? (crotr(w2, 17) ^ crotr(w2, 19) ^ (w2 >> 10))
+                                       : xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wi = w[j16] + s0 + w[j7] + s1;
+            kc[j16] = kc[j16] && kc[j15] && kc[j7] && kc[j2];
+            w[j16] = wi;
+        }
+        uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        uint32_t t1 = add3(add3(h, S1, ch(e, f, g)), K[i], wi);
+        uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        uint32_t mj = maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = add3(t1, S0, mj);
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+// ---------------------------------------------------------------------------
 // Leaf: message word i (big-endian) of 0x00 || ns || share, given the share as
 // big-endian words S[0..127] and `parity` (ns = 0xFF*29 instead of share[0:29]).
 // Block b needs S[16b-8 .. 16b+8].
