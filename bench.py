@@ -558,7 +558,7 @@ def main():
             extras["config5"] = {"error": f"{type(e).__name__}: {e}"}
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
         cpu = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
