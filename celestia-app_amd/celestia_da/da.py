@@ -81,7 +81,20 @@ class DataAvailabilityHeader:
         return self.hash() == other.hash()
 
     def to_proto(self) -> dict:
+        """ToProto (:110-119); the message as a dict of its two fields."""
         return {"row_roots": list(self.row_roots), "column_roots": list(self.column_roots)}
+
+    def marshal(self) -> bytes:
+        """Protobuf wire bytes of celestia.core.v1.da.DataAvailabilityHeader
+        (proto/celestia/core/v1/da/data_availability_header.proto:16-21:
+        repeated bytes row_roots = 1; repeated bytes column_roots = 2)."""
+        out = bytearray()
+        for tag, roots in ((0x0A, self.row_roots), (0x12, self.column_roots)):
+            for r in roots:
+                out.append(tag)
+                out += _uvarint(len(r))
+                out += r
+        return bytes(out)
 
     def validate_basic(self):
         """ValidateBasic (:134-162)."""
@@ -106,11 +119,69 @@ class DataAvailabilityHeader:
 
 
 def data_availability_header_from_proto(p: dict) -> DataAvailabilityHeader:
+    """DataAvailabilityHeaderFromProto (:121-131): copy, then ValidateBasic."""
     if p is None:
         raise ValueError("nil DataAvailabilityHeader")
     d = DataAvailabilityHeader(p.get("row_roots"), p.get("column_roots"))
     d.validate_basic()
     return d
+
+
+def _uvarint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def unmarshal_data_availability_header(buf: bytes) -> dict:
+    """Parse DataAvailabilityHeader wire bytes into the to_proto() dict.
+    Unknown fields are skipped as protobuf requires; malformed input raises
+    ValueError (gogoproto's Unmarshal returns an error)."""
+    p = {"row_roots": [], "column_roots": []}
+    i, n = 0, len(buf)
+
+    def varint():
+        nonlocal i
+        v, shift = 0, 0
+        while True:
+            if i >= n or shift > 63:
+                raise ValueError("proto: unexpected EOF in varint")
+            b = buf[i]
+            i += 1
+            v |= (b & 0x7F) << shift
+            shift += 7
+            if b < 0x80:
+                return v
+
+    while i < n:
+        key = varint()
+        field, wt = key >> 3, key & 7
+        if field == 0:
+            raise ValueError("proto: illegal tag 0")
+        if wt == 2:
+            ln = varint()
+            if i + ln > n:
+                raise ValueError("proto: unexpected EOF in bytes field")
+            val = bytes(buf[i:i + ln])
+            i += ln
+            if field == 1:
+                p["row_roots"].append(val)
+            elif field == 2:
+                p["column_roots"].append(val)
+        elif field in (1, 2):
+            raise ValueError(f"proto: wrong wireType = {wt} for field {field}")
+        elif wt == 0:
+            varint()
+        elif wt == 1 or wt == 5:
+            i += 8 if wt == 1 else 4
+            if i > n:
+                raise ValueError("proto: unexpected EOF")
+        else:
+            raise ValueError(f"proto: illegal wireType {wt}")
+    return p
 
 
 def new_data_availability_header(eds: rsmt2d.ExtendedDataSquare) -> DataAvailabilityHeader:
