@@ -173,6 +173,7 @@ class Engine {
     // Batch pipeline: RS of chunk i+1 (HBM/VALU mix) overlaps the SHA-256
     // stages of chunk i (VALU) on a second stream.
     hipStream_t rs_stream_ = nullptr, hash_stream_ = nullptr;
+    bool cu_split_ = false;   // CDA_RS_CU: RS and hash streams on disjoint CU masks
     std::vector<hipEvent_t> sync_events_;
     uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
     hipEvent_t sync_event(size_t i);

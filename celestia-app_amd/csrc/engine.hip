@@ -84,13 +84,45 @@ int Engine::init() {
     if ((rc = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority), so RS workgroups win free CU slots.
-    if (const char* env = getenv("CDA_RS_PRIORITY")) {
+    // CDA_RS_CU=S:R[:G] (tuning): spatial split of the pipeline's streams.  CU
+    // mask bit i goes to the RS stream when (i / G) % S < R (G defaults to 8,
+    // so the split is even whether the driver stripes mask bits over the 8
+    // XCDs or numbers each XCD's CUs contiguously); the hash stream gets the
+    // complement unless CDA_HASH_ALL_CUS=1.  RS is HBM/latency-bound with one
+    // workgroup per CU, SHA-256 VALU-bound: on disjoint CUs they co-run without
+    // fighting over one CU's VGPRs and LDS.
+    const char* cu_env = getenv("CDA_RS_CU");
+    if (cu_env) {
+        unsigned S = 8, R = 1, G = 8;
+        if (sscanf(cu_env, "%u:%u:%u", &S, &R, &G) < 2 || S == 0 || G == 0 || R >= S)
+            return fail(CDA_ERR_INVALID, "CDA_RS_CU must be S:R[:G] with 0 < R < S");
+        int ncu = 0;
+        if ((rc = check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_),
+                        "hipDeviceGetAttribute")))
+            return rc;
+        const uint32_t words = (uint32_t)(ncu + 31) / 32;
+        std::vector<uint32_t> rs_mask(words, 0), hash_mask(words, 0);
+        for (int i = 0; i < ncu; i++) {
+            const bool rs = (i / G) % S < R;
+            (rs ? rs_mask : hash_mask)[i / 32] |= 1u << (i % 32);
+        }
+        if (getenv("CDA_HASH_ALL_CUS"))
+            for (int i = 0; i < ncu; i++) hash_mask[i / 32] |= 1u << (i % 32);
+        if ((rc = check(hipExtStreamCreateWithCUMask(&rs_stream_, words, rs_mask.data()), "hipExtStreamCreateWithCUMask")))
+            return rc;
+        if ((rc = check(hipExtStreamCreateWithCUMask(&hash_stream_, words, hash_mask.data()),
+                        "hipExtStreamCreateWithCUMask")))
+            return rc;
+        cu_split_ = true;
+    } else if (const char* env = getenv("CDA_RS_PRIORITY")) {
         if ((rc = check(hipStreamCreateWithPriority(&rs_stream_, hipStreamNonBlocking, atoi(env)), "hipStreamCreate")))
             return rc;
     } else if ((rc = check(hipStreamCreateWithFlags(&rs_stream_, hipStreamNonBlocking), "hipStreamCreate"))) {
         return rc;
     }
-    if ((rc = check(hipStreamCreateWithFlags(&hash_stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if (!hash_stream_ &&
+        (rc = check(hipStreamCreateWithFlags(&hash_stream_, hipStreamNonBlocking), "hipStreamCreate")))
+        return rc;
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
@@ -374,10 +406,16 @@ int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uin
     for (uint32_t i = 0; i < n_chunks; i++) {
         const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
         uint8_t* eds = d_eds + i0 * eds_sq;
-        if ((rc = enqueue_extend(d_ods + i0 * ods_sq, k, m, eds, rs_stream_))) return rc;
-        hipEvent_t ev = sync_event(1 + i);
-        if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
-        if ((rc = check(hipStreamWaitEvent(hash_stream_, ev, 0), "hipStreamWaitEvent"))) return rc;
+        // With a CU split the first chunk's RS runs on the hash stream's CUs
+        // (they have nothing else to do yet) instead of the small RS subset.
+        if (i == 0 && cu_split_) {
+            if ((rc = enqueue_extend(d_ods, k, m, eds, hash_stream_))) return rc;
+        } else {
+            if ((rc = enqueue_extend(d_ods + i0 * ods_sq, k, m, eds, rs_stream_))) return rc;
+            hipEvent_t ev = sync_event(1 + i);
+            if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
+            if ((rc = check(hipStreamWaitEvent(hash_stream_, ev, 0), "hipStreamWaitEvent"))) return rc;
+        }
         if ((rc = enqueue_dah(eds, k, m, d_rows + (size_t)i0 * W * kNode, d_cols + (size_t)i0 * W * kNode,
                               d_roots + (size_t)i0 * 32, d_err + i0, d_status ? d_status + i0 : nullptr,
                               hash_stream_)))
