@@ -32,6 +32,15 @@ PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.
 # on this ISA); `achieved_instr` reports the raw instruction rate.
 SHA_INSTR = 1384
 SHA_SLOTS = 2182
+# Achievable ceilings (measured, not spec): tools/sha_probe.hip runs the same
+# sha_compress stream on registers only -- 28.45 G compressions/s at 4
+# waves/SIMD (profiles/r01f_sha_probe.txt), because gfx950 issues a mixed
+# half-rate / full-rate stream at about the half rate (64 lane-ops/clk/CU,
+# profiles/r01f_valu_probe.txt "alignbit+xor"); HBM 6.29 TB/s float4 copy
+# (MI355X_MICROARCH.md).  Reported beside the spec peak as `achievable`.
+ACHIEVABLE_SHA_COMP_S = 28.453e9
+ACHIEVABLE_VALU_TOPS = ACHIEVABLE_SHA_COMP_S * SHA_SLOTS / 1e12
+ACHIEVABLE_HBM_GBS = 6290.0
 SHARE = 512
 
 
@@ -67,6 +76,9 @@ def stage_report(st: dict, k: int, batch: int) -> dict:
             rec.update(bound="hbm", achieved=byt / (avg * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
         if "achieved" in rec:
             rec["frac"] = rec["achieved"] / rec["peak"]
+            ach = ACHIEVABLE_VALU_TOPS if rec["bound"] == "valu" else ACHIEVABLE_HBM_GBS
+            rec["achievable"] = ach
+            rec["frac_of_achievable"] = rec["achieved"] / ach
         out[name] = rec
     return out
 
@@ -461,11 +473,14 @@ def main():
     dom = max((s for s in stages if "achieved" in stages[s]), key=lambda s: stages[s]["avg_ms"])
     d = stages[dom]
     roofline = {"bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"], "unit": d["unit"],
-                "frac": d["frac"], "traffic": load_traffic(dom), "kernel": dom}
+                "frac": d["frac"], "traffic": load_traffic(dom), "kernel": dom,
+                "achievable": d["achievable"], "frac_of_achievable": d["frac_of_achievable"]}
     rs_ms = sum(stages[s]["avg_ms"] for s in ("rs_q0", "rs_q3") if s in stages)
     rs_roof = {"bound": "hbm", "achieved": rs_bytes(k) * B / (rs_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                "unit": "GB/s"}
     rs_roof["frac"] = rs_roof["achieved"] / rs_roof["peak"]
+    rs_roof["achievable"] = ACHIEVABLE_HBM_GBS
+    rs_roof["frac_of_achievable"] = rs_roof["achieved"] / ACHIEVABLE_HBM_GBS
 
     extras = {}
     if rank == 0 and not args.no_extras:
