@@ -57,7 +57,7 @@ def rs_bytes(k: int) -> int:
     return 4 * k * k * SHARE                     # ODS read + 3 parity quadrants written
 
 
-def stage_report(st: dict, k: int, batch: int) -> dict:
+def stage_report(st: dict, k: int, batch: int, inplace: bool = False) -> dict:
     out = {}
     comp = compressions(k)
     for name, (ms, n) in st.items():
@@ -72,7 +72,8 @@ def stage_report(st: dict, k: int, batch: int) -> dict:
                        compressions_per_s=c / (avg * 1e-3))
         elif name in ("rs_q0", "rs_q3"):
             # rs_q0: read ODS, write Q0|Q1|Q2 (4 k^2 shares); rs_q3: read Q2, write Q3 (2 k^2 shares)
-            byt = (4 if name == "rs_q0" else 2) * k * k * SHARE * batch
+            # (in place there is no Q0 copy: read Q0, write Q1|Q2 = 3 k^2 shares)
+            byt = ((3 if inplace else 4) if name == "rs_q0" else 2) * k * k * SHARE * batch
             rec.update(bound="hbm", achieved=byt / (avg * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
         if "achieved" in rec:
             rec["frac"] = rec["achieved"] / rec["peak"]
@@ -402,6 +403,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip k=512 and latency extras")
+    ap.add_argument("--layout", choices=("packed", "inplace"), default="packed",
+                    help="packed: ODS in its own k*k buffer (cda_extend_dah_device, Q0 copied into the EDS); "
+                         "inplace: ODS already in Q0 of the EDS (cda_extend_dah_inplace_device)")
     args = ap.parse_args()
 
     import numpy as np
@@ -434,9 +438,18 @@ def main():
     d_status = torch.empty(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step():
-        ctx.extend_dah_device(d_ods.data_ptr(), k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
-                              d_roots.data_ptr(), d_status.data_ptr(), stream)
+    if args.layout == "inplace":
+        # the ODS arrives in Q0 of the EDS arena (cda_extend_dah_inplace_device)
+        d_eds.view(B, W, W, SHARE)[:, :k, :k] = d_ods.view(B, k, k, SHARE)
+        del d_ods
+
+        def step():
+            ctx.extend_dah_inplace_device(k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
+                                          d_roots.data_ptr(), d_status.data_ptr(), stream)
+    else:
+        def step():
+            ctx.extend_dah_device(d_ods.data_ptr(), k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
+                                  d_roots.data_ptr(), d_status.data_ptr(), stream)
 
     for _ in range(args.warmup):
         step()
@@ -469,7 +482,7 @@ def main():
 
     total_sq = B * world * args.steps
     value = total_sq / el
-    stages = stage_report(st, k, B)
+    stages = stage_report(st, k, B, args.layout == "inplace")
     dom = max((s for s in stages if "achieved" in stages[s]), key=lambda s: stages[s]["avg_ms"])
     d = stages[dom]
     roofline = {"bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"], "unit": d["unit"],
@@ -592,7 +605,8 @@ def main():
             "data": "synthetic random-namespace squares (testfactory mirror, SplitMix64)",
             "config": {"workload": f"k={k} ODS batch: {B} squares per GPU per step "
                                    f"(config 2 shape; x8 GPUs = config 4's 1024)",
-                       "k": k, "squares_per_gpu_per_step": B, "parallelism": f"dp{world} (independent squares)"},
+                       "k": k, "squares_per_gpu_per_step": B, "parallelism": f"dp{world} (independent squares)",
+                       "layout": args.layout},
             "ods_gb_per_s": value * k * k * SHARE / 1e9,
             "roofline": roofline,
             "rs_roofline": rs_roof,

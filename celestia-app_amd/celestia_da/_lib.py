@@ -39,6 +39,7 @@ CDA_SQUARE_BUILD = 1
 EXPORTED = (
     "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
     "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
+    "cda_extend_dah_inplace_device",
     "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
@@ -110,6 +111,7 @@ def load():
         L.cda_extend_dah_batch.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p, u8p,
                                            C.POINTER(C.c_int32)]
         L.cda_extend_dah_device.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.cda_extend_dah_inplace_device.argtypes = [ctxp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.cda_rs_encode.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
         L.cda_data_root.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p]
         L.cda_push_order_detail.argtypes = [ctxp, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
@@ -203,6 +205,12 @@ class Context:
         """Enqueue the whole path on device pointers (asynchronous)."""
         self.check(self.lib.cda_extend_dah_device(self.h, d_ods, k, n, d_eds, d_rows, d_cols, d_roots,
                                                   d_status, stream))
+
+    def extend_dah_inplace_device(self, k: int, n: int, d_eds: int, d_rows: int, d_cols: int, d_roots: int,
+                                  d_status: int | None = None, stream: int | None = None):
+        """As extend_dah_device with the ODS already in Q0 of d_eds (asynchronous)."""
+        self.check(self.lib.cda_extend_dah_inplace_device(self.h, k, n, d_eds, d_rows, d_cols, d_roots,
+                                                          d_status, stream))
 
     # -- config 5 (one square split across ranks); device pointers as ints --
     def split_rows(self, d_rows, k, n_rows, row0, d_block, d_err, stream=None):

@@ -151,6 +151,22 @@ int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t 
     });
 }
 
+int cda_extend_dah_inplace_device(cda_ctx* ctx, uint32_t k, uint32_t n, void* d_eds, void* d_row_roots,
+                                  void* d_col_roots, void* d_data_roots, int32_t* d_status, void* stream) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (k == 0 || (k & (k - 1))) return not_pow2(e, k * k);
+        if (n == 0) return CDA_OK;
+        if (!d_eds || !d_row_roots || !d_col_roots || !d_data_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
+        static thread_local cda::DevBuf err;
+        hipError_t he = err.ensure((size_t)n * 4);
+        if (he != hipSuccess) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        return e.enqueue_extend_dah(nullptr, k, n, static_cast<uint8_t*>(d_eds), static_cast<uint8_t*>(d_row_roots),
+                                    static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_data_roots),
+                                    err.as<uint32_t>(), d_status, s);
+    });
+}
+
 int cda_rs_encode(cda_ctx* ctx, const uint8_t* data, uint32_t n_shards, uint32_t shard_len, uint32_t n_codewords,
                   uint8_t* parity) {
     return guarded(ctx, [&](cda::Engine& e) -> int {

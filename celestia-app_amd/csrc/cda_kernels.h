@@ -54,6 +54,7 @@ hipError_t launch_rs16_flat(const Gf16Dev& t, const uint8_t* data, uint8_t* pari
 // Square phases (rsmt2d erasureExtendSquare): Q0->Q1 rows + Q0->Q2 columns
 // (with the Q0 copy), then Q2->Q3 rows.
 RsJob square_job_q0(const uint8_t* ods, uint8_t* eds, uint32_t k);
+RsJob square_job_q0_inplace(uint8_t* eds, uint32_t k);
 RsJob square_job_q3(uint8_t* eds, uint32_t k);
 
 // A grid of EDS cells seen by the hash kernels: cell (r, c) of square y at

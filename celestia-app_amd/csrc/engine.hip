@@ -219,7 +219,9 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
     int rc;
     const Gf16Dev t = gf16(k);
     mark_begin(kStageRsQ0, s);
-    if ((rc = check(launch_rs(square_job_q0(d_ods, d_eds, k), k, n, t, s), "rs Q0"))) return rc;
+    // d_ods == NULL: in place, the ODS is already in Q0 of d_eds
+    const RsJob q0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
+    if ((rc = check(launch_rs(q0, k, n, t, s), "rs Q0"))) return rc;
     mark_end(s);
     mark_begin(kStageRsQ3, s);
     if ((rc = check(launch_rs(square_job_q3(d_eds, k), k, n, t, s), "rs Q3"))) return rc;
@@ -411,7 +413,7 @@ int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uin
         if (i == 0 && cu_split_) {
             if ((rc = enqueue_extend(d_ods, k, m, eds, hash_stream_))) return rc;
         } else {
-            if ((rc = enqueue_extend(d_ods + i0 * ods_sq, k, m, eds, rs_stream_))) return rc;
+            if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, eds, rs_stream_))) return rc;
             hipEvent_t ev = sync_event(1 + i);
             if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
             if ((rc = check(hipStreamWaitEvent(hash_stream_, ev, 0), "hipStreamWaitEvent"))) return rc;

@@ -224,6 +224,22 @@ RsJob square_job_q0(const uint8_t* ods, uint8_t* eds, uint32_t k) {
     return j;
 }
 
+// In place: the ODS already sits in Q0 of the EDS (cda_extend_dah_inplace_*),
+// so both segments read Q0 at the EDS row stride and nothing is copied.
+RsJob square_job_q0_inplace(uint8_t* eds, uint32_t k) {
+    const uint32_t W = 2 * k, SH = 512;
+    RsJob j{};
+    j.src = eds;
+    j.dst = eds;
+    j.src_sq = j.dst_sq = (uint64_t)W * W * SH;
+    j.n_seg = 2;
+    // rows: Q0 row c -> Q1 row c
+    j.seg[0] = RsSeg{k, 0, W * SH, SH, k * SH, W * SH, SH};
+    // columns: Q0 column c -> Q2 column c
+    j.seg[1] = RsSeg{k, 0, SH, W * SH, k * W * SH, SH, W * SH};
+    return j;
+}
+
 RsJob square_job_q3(uint8_t* eds, uint32_t k) {
     const uint32_t W = 2 * k, SH = 512;
     RsJob j{};

@@ -21,6 +21,9 @@
  *   cda_data_root          (*DataAvailabilityHeader).Hash
  *                          pkg/da/data_availability_header.go:92-108
  *   cda_extend_dah_device  device-resident batch (inputs/outputs in HBM)
+ *   cda_extend_dah_inplace_device
+ *                          the same with the ODS already in Q0 of the EDS
+ *                          (rsmt2d ImportExtendedDataSquare-style arena)
  *   cda_square_layout / cda_square_construct / cda_construct_extend_dah /
  *   cda_square_construct_device
  *                          go-square square.Construct / square.Build (EXT
@@ -119,6 +122,15 @@ int cda_extend_dah_batch(cda_ctx *ctx, const uint8_t *ods, uint32_t k, uint32_t 
  * (n int32, device memory, may be NULL). */
 int cda_extend_dah_device(cda_ctx *ctx, const void *d_ods, uint32_t k, uint32_t n, void *d_eds, void *d_row_roots,
                           void *d_col_roots, void *d_data_roots, int32_t *d_status, void *stream);
+
+/* As cda_extend_dah_device, but the k*k ODS shares are already in place in
+ * quadrant Q0 of d_eds (row r, column c at (r*2k + c)*512 of each square),
+ * the layout rsmt2d's EDS has after ExtendShares.  The cgo caller flattens the
+ * [][]byte shares straight into that arena (it must copy them into one flat
+ * buffer anyway), so the kernels read Q0 where it lies and never copy it.
+ * Outputs and semantics are identical to cda_extend_dah_device. */
+int cda_extend_dah_inplace_device(cda_ctx *ctx, uint32_t k, uint32_t n, void *d_eds, void *d_row_roots,
+                                  void *d_col_roots, void *d_data_roots, int32_t *d_status, void *stream);
 
 /* rsmt2d Codec.Encode (Leopard, GF(2^8) for 2*n_shards <= 256, else GF(2^16)):
  * n_codewords codewords, each n_shards data shards of shard_len bytes,

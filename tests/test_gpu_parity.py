@@ -168,3 +168,43 @@ def test_split_push_order_on_gpu(ctx):
     _, (_, _, _, err) = cdist.extend_dah_split_loopback(torch.from_numpy(ods.reshape(-1, 512)).to(dev), k, 4,
                                                          cdist.GpuSplitOps(ctx, dev))
     assert int(err.item()) == (0 << 24) | (5 << 12) | 10
+
+
+@pytest.mark.parametrize("k,n", [(1, 2), (2, 3), (16, 2), (64, 2), (128, 3), (256, 1), (512, 1)])
+def test_inplace_device_matches_device_entry(ctx, k, n):
+    """cda_extend_dah_inplace_device (ODS already in Q0 of the EDS, no copy)
+    gives the same EDS, roots, data roots and status as cda_extend_dah_device
+    on the same squares; the last square is checked against the oracle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    W = 2 * k
+    ods = np.stack([coracle.random_square(k, 40 + i) for i in range(n)])
+    if n > 1 and k >= 2:   # one square out of namespace order -> status set, bytes still equal
+        sq = ods[0].reshape(k, k, 512)
+        sq[0, 0, :29], sq[0, 1, :29] = sq[0, 1, :29].copy(), sq[0, 0, :29].copy()
+    d_ods = torch.from_numpy(ods.reshape(n, k * k * 512)).to(dev)
+
+    def outs():
+        return (torch.zeros(n, W * W * 512, dtype=torch.uint8, device=dev),
+                torch.empty(n, W * 90, dtype=torch.uint8, device=dev),
+                torch.empty(n, W * 90, dtype=torch.uint8, device=dev),
+                torch.empty(n, 32, dtype=torch.uint8, device=dev),
+                torch.empty(n, dtype=torch.int32, device=dev))
+
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    a = outs()
+    ctx.extend_dah_device(d_ods.data_ptr(), k, n, *[t.data_ptr() for t in a], stream)
+    b = outs()
+    b[0].view(n, W, W, 512)[:, :k, :k] = d_ods.view(n, k, k, 512)
+    ctx.extend_dah_inplace_device(k, n, *[t.data_ptr() for t in b], stream)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    if k <= 128:
+        e_eds, e_rows, e_cols, e_root = coracle.extend_dah(ods[-1])
+        assert np.array_equal(b[0][-1].cpu().numpy().reshape(-1, 512), e_eds)
+        assert b[3][-1].cpu().numpy().tobytes() == e_root
+    status = b[4].cpu().numpy()
+    assert (status[1:] == 0).all()
+    if n > 1 and k >= 2:
+        assert status[0] != 0
