@@ -493,6 +493,10 @@ def main():
                "unit": "GB/s"}
     rs_roof["frac"] = rs_roof["achieved"] / rs_roof["peak"]
     rs_roof["achievable"] = ACHIEVABLE_HBM_GBS
+    # measured HBM bytes of the two RS launches of one step (PMC summary, the
+    # per-launch mean over rs_q0 and rs_q3), against rs_bytes(k) * B algorithmic
+    t_rs = load_traffic("rs_gf8_bs" if k == 128 else "rs_gf16")
+    rs_roof["traffic"] = 2 * t_rs if t_rs else None
     rs_roof["frac_of_achievable"] = rs_roof["achieved"] / ACHIEVABLE_HBM_GBS
 
     extras = {}
