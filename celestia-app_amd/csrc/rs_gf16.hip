@@ -68,6 +68,11 @@ __device__ __forceinline__ void mul_add16(uint32_t& xl, uint32_t& xh, uint32_t y
     xh = xor3(xh, perm1(tab[13], h2), perm1(tab[15], h3));
 }
 
+__device__ __forceinline__ void mul_add16(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh,
+                                          const uint32_t (&tab)[16]) {
+    mul_add16(xl, xh, yl, yh, static_cast<const uint32_t*>(tab));
+}
+
 // tab layout: [skew index][16 dwords].  A skew equal to the modulus means
 // "multiply by zero" (leopard skips the multiply); its tables are all zero, so
 // the butterfly stays branch-free and bit-identical.
@@ -101,39 +106,98 @@ __device__ __forceinline__ void sfor(F&& f) {
 // In-register IFFT / FFT layers over N consecutive registers holding shards
 // base + i*stride_abs; constant index of group g (register space) is
 // IDX(g, d) (uniform).
+//
+// The N-1 butterfly groups of the layers run as one flat sequence whose
+// table loads are software-pipelined: group I first waits for its own 16
+// table dwords (loaded while group I-1 computed; the inline-asm SGPR use is
+// where the wait lands), then issues the scalar load of group I+1's tables,
+// then runs its butterflies.  Scalar loads return out of order, so waiting
+// for one means waiting for all: issuing the next load only after the wait
+// keeps it in flight across a whole group.  CDA_RS16_NO_PREFETCH restores
+// load-then-use per group.
+template <int N, bool INV>
+constexpr int grp_at(int I, bool want_d) {
+    for (int l = 0; l < 16; l++) {
+        const int d = INV ? (1 << l) : ((N / 2) >> l);
+        if (d < 1 || d >= N) break;
+        const int ng = N / (2 * d);
+        if (I < ng) return want_d ? d : 2 * d * I;
+        I -= ng;
+    }
+    return -1;
+}
+
+template <int B, int E, int N>
+__device__ __forceinline__ void launder(uint32_t (&lo)[N], uint32_t (&hi)[N]) {
+    if constexpr (B < E) {
+        asm volatile("" : "+v"(lo[B]), "+v"(hi[B]));
+        launder<B + 1, E>(lo, hi);
+    }
+}
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+// 16 table dwords into SGPRs (a scalar-cache read; the caller waits).
+__device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
+    u32x16 v;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+
+template <int N, bool INV, class IdxF>
+__device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
+    constexpr int NG = N - 1;
+#ifdef CDA_RS16_NO_PREFETCH
+    sfor<0, NG, 1>([&](auto II) {
+        constexpr int g = grp_at<N, INV>(decltype(II)::value, false), d = grp_at<N, INV>(decltype(II)::value, true);
+        const uint32_t idx = idxf(g, d);
+        asm volatile("" ::: "memory");   // one constant's tables in SGPRs at a time
+        sfor<g, g + d, 1>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            if constexpr (INV) ifft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
+            else fft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
+        });
+    });
+#else
+    // The scalar loads are issued from inline asm: the compiler treats loads
+    // of the (invariant) tables as freely movable and would sink a plain load
+    // back next to its first use.  The wait is explicit for the same reason.
+    u32x16 tc = sload16(T.t + (size_t)idxf(grp_at<N, INV>(0, false), grp_at<N, INV>(0, true)) * 16);
+    sfor<0, NG, 1>([&](auto II) {
+        constexpr int I = decltype(II)::value;
+        constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc)::"memory");   // this group's tables are here
+        u32x16 tn;
+        if constexpr (I + 1 < NG)
+            tn = sload16(T.t + (size_t)idxf(grp_at<N, INV>(I + 1, false), grp_at<N, INV>(I + 1, true)) * 16);
+        // the group's operands pass through volatile asm after the load, so
+        // the scheduler cannot hoist the butterflies above it
+        launder<g, g + 2 * d>(lo, hi);
+        uint32_t t[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) t[j] = tc[j];
+        sfor<g, g + d, 1>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            if constexpr (INV) {
+                hi[i + d] ^= hi[i];
+                lo[i + d] ^= lo[i];
+                mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
+            } else {
+                mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
+                lo[i + d] ^= lo[i];
+                hi[i + d] ^= hi[i];
+            }
+        });
+        if constexpr (I + 1 < NG) tc = tn;
+    });
+#endif
+}
 template <int N, class IdxF>
 __device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
-    sfor<0, 8, 1>([&](auto ld) {
-        constexpr int d = 1 << decltype(ld)::value;
-        if constexpr (d < N) {
-            sfor<0, N, 2 * d>([&](auto gg) {
-                constexpr int g = decltype(gg)::value;
-                const uint32_t idx = idxf(g, d);
-                asm volatile("" ::: "memory");   // one constant's tables in SGPRs at a time
-                sfor<g, g + d, 1>([&](auto ii) {
-                    constexpr int i = decltype(ii)::value;
-                    ifft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
-                });
-            });
-        }
-    });
+    layers_regs<N, true>(lo, hi, T, idxf);
 }
 template <int N, class IdxF>
 __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
-    sfor<0, 8, 1>([&](auto ld) {
-        constexpr int d = (N / 2) >> decltype(ld)::value;
-        if constexpr (d >= 1) {
-            sfor<0, N, 2 * d>([&](auto gg) {
-                constexpr int g = decltype(gg)::value;
-                const uint32_t idx = idxf(g, d);
-                asm volatile("" ::: "memory");
-                sfor<g, g + d, 1>([&](auto ii) {
-                    constexpr int i = decltype(ii)::value;
-                    fft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
-                });
-            });
-        }
-    });
+    layers_regs<N, false>(lo, hi, T, idxf);
 }
 
 constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
