@@ -6,7 +6,8 @@ Mirrors /root/reference/pkg/da/data_availability_header_test.go:
     also through the protobuf wire bytes of
     proto/celestia/core/v1/da/data_availability_header.proto:16-21;
   * Test_DAHValidateBasic (:135-215): min / max pass; too big, too small,
-    bad hash and mismatched root counts fail with the reference's messages.
+    bad hash and mismatched root counts fail with the reference's messages;
+  * TestSquareSize (:217-245).
 The wire format and the size checks are host logic (CPU); everything that
 hashes roots runs on the GPU (libcda.so).
 """
@@ -74,6 +75,9 @@ def test_proto_conversion_min_max(ctx):
     shares = pyref.constant_shares(128 * 128)      # generateShares(maxSize), :247-263 shape
     big = da.new_data_availability_header(da.extend_shares(shares))
     big.validate_basic()
+    # TestSquareSize (:217-245): min -> 1, max -> DefaultSquareSizeUpperBound
+    assert da.min_data_availability_header().square_size() == 1
+    assert big.square_size() == da.DEFAULT_SQUARE_SIZE_UPPER_BOUND
     for dah in (da.min_data_availability_header(), big):
         res = da.data_availability_header_from_proto(dah.to_proto())
         assert res.row_roots == dah.row_roots and res.column_roots == dah.column_roots
