@@ -143,51 +143,87 @@ __device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
     return v;
 }
 
-template <int N, bool INV, class IdxF>
+// Leopard skips the multiply when the skew is the modulus (log 0).  The FFT
+// skew of index 2^j - 1 is always the modulus (initFFT sets skew[(1<<m)-1] = 0
+// before taking logs), and in pass B every FFT group with gt = 0 has index
+// S*dt - 1: ZERO_G0 drops those multiplies at compile time (480 of the 4 608
+// butterfly multiplies of a k = 512 codeword); their tables are all zero, so
+// the result is bit-identical either way.
+template <int N, bool INV, bool ZERO_G0>
+constexpr bool grp_mul(int I) {
+    return I < N - 1 && !(ZERO_G0 && grp_at<N, INV>(I, false) == 0);
+}
+template <int N, bool INV, bool ZERO_G0>
+constexpr int next_mul(int I) {
+    int J = I + 1;
+    while (J < N - 1 && !grp_mul<N, INV, ZERO_G0>(J)) J++;
+    return J;
+}
+
+template <int N, bool INV, bool ZERO_G0 = false, class IdxF>
 __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
+    static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
 #ifdef CDA_RS16_NO_PREFETCH
     sfor<0, NG, 1>([&](auto II) {
-        constexpr int g = grp_at<N, INV>(decltype(II)::value, false), d = grp_at<N, INV>(decltype(II)::value, true);
-        const uint32_t idx = idxf(g, d);
-        asm volatile("" ::: "memory");   // one constant's tables in SGPRs at a time
-        sfor<g, g + d, 1>([&](auto ii) {
-            constexpr int i = decltype(ii)::value;
-            if constexpr (INV) ifft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
-            else fft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
-        });
+        constexpr int I = decltype(II)::value;
+        constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
+        if constexpr (!grp_mul<N, INV, ZERO_G0>(I)) {
+            sfor<g, g + d, 1>([&](auto ii) {
+                lo[ii.value + d] ^= lo[ii.value];
+                hi[ii.value + d] ^= hi[ii.value];
+            });
+        } else {
+            const uint32_t idx = idxf(g, d);
+            asm volatile("" ::: "memory");   // one constant's tables in SGPRs at a time
+            sfor<g, g + d, 1>([&](auto ii) {
+                constexpr int i = decltype(ii)::value;
+                if constexpr (INV) ifft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
+                else fft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
+            });
+        }
     });
 #else
     // The scalar loads are issued from inline asm: the compiler treats loads
     // of the (invariant) tables as freely movable and would sink a plain load
     // back next to its first use.  The wait is explicit for the same reason.
-    u32x16 tc = sload16(T.t + (size_t)idxf(grp_at<N, INV>(0, false), grp_at<N, INV>(0, true)) * 16);
+    constexpr int F0 = next_mul<N, INV, ZERO_G0>(-1);
+    u32x16 tc{};
+    if constexpr (F0 < NG) tc = sload16(T.t + (size_t)idxf(grp_at<N, INV>(F0, false), grp_at<N, INV>(F0, true)) * 16);
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
         constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc)::"memory");   // this group's tables are here
-        u32x16 tn;
-        if constexpr (I + 1 < NG)
-            tn = sload16(T.t + (size_t)idxf(grp_at<N, INV>(I + 1, false), grp_at<N, INV>(I + 1, true)) * 16);
-        // the group's operands pass through volatile asm after the load, so
-        // the scheduler cannot hoist the butterflies above it
-        launder<g, g + 2 * d>(lo, hi);
-        uint32_t t[16];
+        if constexpr (!grp_mul<N, INV, ZERO_G0>(I)) {
+            sfor<g, g + d, 1>([&](auto ii) {      // multiply by zero: XOR only
+                lo[ii.value + d] ^= lo[ii.value];
+                hi[ii.value + d] ^= hi[ii.value];
+            });
+        } else {
+            constexpr int J = next_mul<N, INV, ZERO_G0>(I);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc)::"memory");   // this group's tables are here
+            u32x16 tn;
+            if constexpr (J < NG)
+                tn = sload16(T.t + (size_t)idxf(grp_at<N, INV>(J, false), grp_at<N, INV>(J, true)) * 16);
+            // the group's operands pass through volatile asm after the load, so
+            // the scheduler cannot hoist the butterflies above it
+            launder<g, g + 2 * d>(lo, hi);
+            uint32_t t[16];
 #pragma unroll
-        for (int j = 0; j < 16; j++) t[j] = tc[j];
-        sfor<g, g + d, 1>([&](auto ii) {
-            constexpr int i = decltype(ii)::value;
-            if constexpr (INV) {
-                hi[i + d] ^= hi[i];
-                lo[i + d] ^= lo[i];
-                mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
-            } else {
-                mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
-                lo[i + d] ^= lo[i];
-                hi[i + d] ^= hi[i];
-            }
-        });
-        if constexpr (I + 1 < NG) tc = tn;
+            for (int j = 0; j < 16; j++) t[j] = tc[j];
+            sfor<g, g + d, 1>([&](auto ii) {
+                constexpr int i = decltype(ii)::value;
+                if constexpr (INV) {
+                    hi[i + d] ^= hi[i];
+                    lo[i + d] ^= lo[i];
+                    mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
+                } else {
+                    mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
+                    lo[i + d] ^= lo[i];
+                    hi[i + d] ^= hi[i];
+                }
+            });
+            if constexpr (J < NG) tc = tn;
+        }
     });
 #endif
 }
@@ -195,9 +231,9 @@ template <int N, class IdxF>
 __device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
     layers_regs<N, true>(lo, hi, T, idxf);
 }
-template <int N, class IdxF>
+template <int N, bool ZERO_G0 = false, class IdxF>
 __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
-    layers_regs<N, false>(lo, hi, T, idxf);
+    layers_regs<N, false, ZERO_G0>(lo, hi, T, idxf);
 }
 
 constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
@@ -296,7 +332,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         uint32_t l16[16], h16[16];
         sfor<0, 16, 1>([&](auto tt) { l16[tt.value] = lo[R * tt.value + q]; h16[tt.value] = hi[R * tt.value + q]; });
         ifft_regs<16>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
-        fft_regs<16>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
+        fft_regs<16, true>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
         sfor<0, 16, 1>([&](auto tt) { lo[R * tt.value + q] = l16[tt.value]; hi[R * tt.value + q] = h16[tt.value]; });
     });
     xchg_b_to_a();
