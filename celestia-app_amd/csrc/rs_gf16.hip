@@ -323,7 +323,14 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     if (c0 != kNoCopy) {
         sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * g.cpy_sh, lo[jj.value], hi[jj.value]); });
     }
-    ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + base; });
+    // `base` is re-laundered per table index (like lane_off) so the compiler
+    // does not precompute all S-1 group addresses up front and spill them
+    auto wave_base = [&]() {
+        uint32_t b = base;
+        asm volatile("" : "+s"(b));
+        return b;
+    };
+    ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); });
     xchg_a_to_b();
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
     // residue R*wave + q: shards R*wave + q + S*t in registers R*t + q
@@ -337,7 +344,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     });
     xchg_b_to_a();
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
-    fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + base; });
+    fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); });
     sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
 }
 
