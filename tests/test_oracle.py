@@ -175,3 +175,42 @@ def test_push_order_detected_by_oracle():
         coracle.extend_dah(ods.reshape(-1, 512))
     with pytest.raises(pyref.PushOrderError):
         pyref.extend_and_dah(ods)
+
+
+def _lagrange_at(F, d, xs_eval):
+    """Vectorised SURVEY A.4 check: P(x) for x in xs_eval, P of degree < k
+    through (k+i, d[i]) over the Cantor-basis field; d is (k, n_symbols)."""
+    k = d.shape[0]
+    mod, log, exp = F.mod, F.log_np, F.exp_np
+    xs = np.arange(k, 2 * k)
+    diff = xs[:, None] ^ xs[None, :]
+    np.fill_diagonal(diff, 1)                        # log 1 = 0 drops j == i
+    den = log[diff].sum(axis=1) % mod               # log prod_{j != i} (xs_i ^ xs_j)
+    nz = d != 0
+    ld = np.where(nz, log[d], 0)
+    out = []
+    for x in xs_eval:
+        lx = log[x ^ xs]                            # x is not a data point: all non-zero
+        lnum = (lx.sum() - lx) % mod                # log prod_{j != i} (x ^ xs_j)
+        coef = (lnum - den) % mod                   # log L_i(x)
+        terms = np.where(nz, exp[(ld + coef[:, None]) % mod], 0)
+        out.append(np.bitwise_xor.reduce(terms, axis=0))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("k", [256, 512])
+def test_gf16_encoder_equals_lagrange_full_size(k):
+    """The GF(2^16) restatement at the sizes the path uses (config 3, k=512),
+    in the real lo/hi shard layout, equals Lagrange interpolation at sampled
+    parity positions: no reference vector exists for GF(2^16),
+    so this is its full-size intrinsic pin; the GPU is pinned to the same
+    restatement by test_gpu_parity.py."""
+    F = pyref.gf16()
+    rng = np.random.default_rng(k)
+    data = rng.integers(0, 256, (k, 64), dtype=np.uint8)
+    par = coracle.leopard_encode(data)
+    sym = lambda b: b[:, :32].astype(np.int64) | (b[:, 32:].astype(np.int64) << 8)   # symbol i = b[i] | b[i+32] << 8
+    xs_eval = [0, 1, 2, k // 2 - 1, k // 2, k - 1]
+    want = _lagrange_at(F, sym(data), xs_eval)
+    got = sym(par)[xs_eval]
+    assert np.array_equal(got, want)
