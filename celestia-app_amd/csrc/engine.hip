@@ -137,18 +137,34 @@ int Engine::init() {
     // 2-bit-chunk v_perm tables for the constants of the k = 256 / 512 schedules
     for (int v = 0; v < 2; v++) {
         const uint32_t k = v == 0 ? 256 : 512, n = 2 * k - 1;
-        std::vector<uint32_t> tab((size_t)n * 16, 0);
+        std::vector<uint32_t> tab((size_t)n * kGf16TabWords, 0);
         for (uint32_t idx = 0; idx < n; idx++) {
             const uint32_t L = F->skew[idx];
             if (L == LeoField<16>::MOD) continue;    // multiply by zero: all-zero tables
-            for (uint32_t q = 0; q < 8; q++) {
-                const uint32_t shift = q < 4 ? 2 * q : 8 + 2 * (q - 4);
-                for (uint32_t e = 0; e < 4; e++) {
-                    const uint32_t prod = F->mul_log(e << shift, L);
-                    tab[(size_t)idx * 16 + 2 * q] |= (prod & 0xFFu) << (8 * e);
-                    tab[(size_t)idx * 16 + 2 * q + 1] |= (prod >> 8) << (8 * e);
-                }
+            uint32_t* t = tab.data() + (size_t)idx * kGf16TabWords;
+            // put entry e (product of e << shift) into byte `slot` of dword pair
+            // (lo output byte, hi output byte) at t[w], t[w + 1]
+            auto put = [&](uint32_t w, uint32_t e, uint32_t shift, uint32_t slot) {
+                const uint32_t prod = F->mul_log(e << shift, L);
+                t[w] |= (prod & 0xFFu) << (8 * slot);
+                t[w + 1] |= (prod >> 8) << (8 * slot);
+            };
+#ifdef CDA_RS16_CHUNK2
+            for (uint32_t q = 0; q < 8; q++)   // 2-bit chunk q of the symbol, entries 0..3
+                for (uint32_t e = 0; e < 4; e++) put(2 * q, e, q < 4 ? 2 * q : 8 + 2 * (q - 4), e);
+#else
+            // 3-bit chunks a = 0..3 at bits 0, 3 (lo byte) and 8, 11 (hi byte):
+            // entries 4..7 in t[2a], t[2a+1] (v_perm src0, SGPR), entries
+            // 0..3 in t[12+2a], t[13+2a] (src1, copied to VGPRs); 2-bit chunks at
+            // bits 6 and 14: entries 0..3 in t[8..9] and t[10..11]
+            const uint32_t sh3[4] = {0, 3, 8, 11};
+            for (uint32_t a = 0; a < 4; a++)
+                for (uint32_t e = 0; e < 8; e++) put(e < 4 ? 12 + 2 * a : 2 * a, e, sh3[a], e & 3);
+            for (uint32_t e = 0; e < 4; e++) {
+                put(8, e, 6, e);
+                put(10, e, 14, e);
             }
+#endif
         }
         if ((rc = check(gf16_chunk_[v].ensure(tab.size() * 4), "hipMalloc"))) return rc;
         if ((rc = check(hipMemcpy(gf16_chunk_[v].ptr, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "hipMemcpy")))

@@ -73,25 +73,34 @@ __device__ __forceinline__ void mul_add16(uint32_t& xl, uint32_t& xh, uint32_t y
     mul_add16(xl, xh, yl, yh, static_cast<const uint32_t*>(tab));
 }
 
-// tab layout: [skew index][16 dwords].  A skew equal to the modulus means
+// 3-bit chunks (default layout, kGf16TabWords = 24): a 16-bit symbol splits
+// into chunks at bits 0-2, 3-5, 6-7 of each byte; a 3-bit chunk indexes 8
+// table bytes as v_perm(src0 = entries 4..7 in an SGPR, src1 = entries 0..3 in
+// a VGPR, sel) -- gfx9 VOP3 reads one SGPR, so the four src1 dword pairs are
+// copied to VGPRs once per butterfly group.  Per 4 symbols: 12 perms + 10
+// selector ops + 6 XOR3 (2-bit layout: 16 + 14 + 8).
+__device__ __forceinline__ uint32_t perm2(uint32_t s0, uint32_t s1, uint32_t sel) {
+    return __builtin_amdgcn_perm(s0, s1, sel);
+}
+__device__ __forceinline__ void mul_add16_c3(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh,
+                                             const uint32_t (&t)[12], const uint32_t (&b)[8]) {
+    const uint32_t m7 = 0x07070707u, m3 = 0x03030303u;
+    const uint32_t c0 = yl & m7, c1 = (yl >> 3) & m7, c2 = (yl >> 6) & m3;
+    const uint32_t c3 = yh & m7, c4 = (yh >> 3) & m7, c5 = (yh >> 6) & m3;
+    xl = xor3(xl, perm2(t[0], b[0], c0), perm2(t[2], b[2], c1));
+    xl = xor3(xl, perm1(t[8], c2), perm2(t[4], b[4], c3));
+    xl = xor3(xl, perm2(t[6], b[6], c4), perm1(t[10], c5));
+    xh = xor3(xh, perm2(t[1], b[1], c0), perm2(t[3], b[3], c1));
+    xh = xor3(xh, perm1(t[9], c2), perm2(t[5], b[5], c3));
+    xh = xor3(xh, perm2(t[7], b[7], c4), perm1(t[11], c5));
+}
+
+// tab layout: [skew index][kGf16TabWords dwords].  A skew equal to the modulus means
 // "multiply by zero" (leopard skips the multiply); its tables are all zero, so
 // the butterfly stays branch-free and bit-identical.
 struct Tab16 {
     const uint32_t* __restrict__ t;      // [2k-1][16]
 };
-
-__device__ __forceinline__ void ifft_bfly(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const Tab16& T,
-                                          uint32_t idx) {
-    yl ^= xl;
-    yh ^= xh;
-    mul_add16(xl, xh, yl, yh, T.t + (size_t)idx * 16);
-}
-__device__ __forceinline__ void fft_bfly(uint32_t& xl, uint32_t& xh, uint32_t& yl, uint32_t& yh, const Tab16& T,
-                                         uint32_t idx) {
-    mul_add16(xl, xh, yl, yh, T.t + (size_t)idx * 16);
-    yl ^= xl;
-    yh ^= xh;
-}
 
 // Compile-time loops (full unroll with constant register indices: no
 // s_set_gpr_idx register indexing, no scratch).
@@ -108,13 +117,12 @@ __device__ __forceinline__ void sfor(F&& f) {
 // IDX(g, d) (uniform).
 //
 // The N-1 butterfly groups of the layers run as one flat sequence whose
-// table loads are software-pipelined: group I first waits for its own 16
-// table dwords (loaded while group I-1 computed; the inline-asm SGPR use is
-// where the wait lands), then issues the scalar load of group I+1's tables,
-// then runs its butterflies.  Scalar loads return out of order, so waiting
-// for one means waiting for all: issuing the next load only after the wait
-// keeps it in flight across a whole group.  CDA_RS16_NO_PREFETCH restores
-// load-then-use per group.
+// table loads are software-pipelined: group I first waits for its own table
+// dwords (loaded while group I-1 computed; the inline-asm wait), then issues
+// the scalar loads of the next multiplying group's tables, then runs its
+// butterflies.  Scalar loads return out of order, so waiting for one means
+// waiting for all: issuing the next load only after the wait keeps it in
+// flight across a whole group.
 template <int N, bool INV>
 constexpr int grp_at(int I, bool want_d) {
     for (int l = 0; l < 16; l++) {
@@ -136,11 +144,32 @@ __device__ __forceinline__ void launder(uint32_t (&lo)[N], uint32_t (&hi)[N]) {
 }
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 // 16 table dwords into SGPRs (a scalar-cache read; the caller waits).
 __device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
     u32x16 v;
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
     return v;
+}
+__device__ __forceinline__ u32x8 sload8_at64(const uint32_t* p) {   // dwords 16..23
+    u32x8 v;
+    asm volatile("s_load_dwordx8 %0, %1, 0x40" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+// one constant's tables: 16 dwords (+ 8 with the 3-bit layout)
+struct TabRegs {
+    u32x16 a;
+#ifndef CDA_RS16_CHUNK2
+    u32x8 b;
+#endif
+};
+__device__ __forceinline__ TabRegs load_tabs(const uint32_t* p) {
+    TabRegs r;
+    r.a = sload16(p);
+#ifndef CDA_RS16_CHUNK2
+    r.b = sload8_at64(p);
+#endif
+    return r;
 }
 
 // Leopard skips the multiply when the skew is the modulus (log 0).  The FFT
@@ -164,32 +193,15 @@ template <int N, bool INV, bool ZERO_G0 = false, class IdxF>
 __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
     static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
-#ifdef CDA_RS16_NO_PREFETCH
-    sfor<0, NG, 1>([&](auto II) {
-        constexpr int I = decltype(II)::value;
-        constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
-        if constexpr (!grp_mul<N, INV, ZERO_G0>(I)) {
-            sfor<g, g + d, 1>([&](auto ii) {
-                lo[ii.value + d] ^= lo[ii.value];
-                hi[ii.value + d] ^= hi[ii.value];
-            });
-        } else {
-            const uint32_t idx = idxf(g, d);
-            asm volatile("" ::: "memory");   // one constant's tables in SGPRs at a time
-            sfor<g, g + d, 1>([&](auto ii) {
-                constexpr int i = decltype(ii)::value;
-                if constexpr (INV) ifft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
-                else fft_bfly(lo[i], hi[i], lo[i + d], hi[i + d], T, idx);
-            });
-        }
-    });
-#else
     // The scalar loads are issued from inline asm: the compiler treats loads
     // of the (invariant) tables as freely movable and would sink a plain load
     // back next to its first use.  The wait is explicit for the same reason.
+    auto tab_ptr = [&](int I) {
+        return T.t + (size_t)idxf(grp_at<N, INV>(I, false), grp_at<N, INV>(I, true)) * kGf16TabWords;
+    };
     constexpr int F0 = next_mul<N, INV, ZERO_G0>(-1);
-    u32x16 tc{};
-    if constexpr (F0 < NG) tc = sload16(T.t + (size_t)idxf(grp_at<N, INV>(F0, false), grp_at<N, INV>(F0, true)) * 16);
+    TabRegs tc{};
+    if constexpr (F0 < NG) tc = load_tabs(tab_ptr(F0));
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
         constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
@@ -200,24 +212,44 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N]
             });
         } else {
             constexpr int J = next_mul<N, INV, ZERO_G0>(I);
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc)::"memory");   // this group's tables are here
-            u32x16 tn;
-            if constexpr (J < NG)
-                tn = sload16(T.t + (size_t)idxf(grp_at<N, INV>(J, false), grp_at<N, INV>(J, true)) * 16);
+#ifdef CDA_RS16_CHUNK2
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc.a)::"memory");   // this group's tables are here
+#else
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc.a), "+s"(tc.b)::"memory");
+#endif
+            TabRegs tn;
+            if constexpr (J < NG) tn = load_tabs(tab_ptr(J));
             // the group's operands pass through volatile asm after the load, so
             // the scheduler cannot hoist the butterflies above it
             launder<g, g + 2 * d>(lo, hi);
+#ifdef CDA_RS16_CHUNK2
             uint32_t t[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) t[j] = tc[j];
+            for (int j = 0; j < 16; j++) t[j] = tc.a[j];
+#else
+            uint32_t t[12], bv[8];
+#pragma unroll
+            for (int j = 0; j < 12; j++) t[j] = tc.a[j];
+#pragma unroll
+            for (int j = 0; j < 4; j++) asm volatile("v_mov_b32 %0, %1" : "=v"(bv[j]) : "s"(tc.a[12 + j]));
+#pragma unroll
+            for (int j = 0; j < 4; j++) asm volatile("v_mov_b32 %0, %1" : "=v"(bv[4 + j]) : "s"(tc.b[j]));
+#endif
+            auto mul = [&](uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh) {
+#ifdef CDA_RS16_CHUNK2
+                mul_add16(xl, xh, yl, yh, t);
+#else
+                mul_add16_c3(xl, xh, yl, yh, t, bv);
+#endif
+            };
             sfor<g, g + d, 1>([&](auto ii) {
                 constexpr int i = decltype(ii)::value;
                 if constexpr (INV) {
                     hi[i + d] ^= hi[i];
                     lo[i + d] ^= lo[i];
-                    mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
+                    mul(lo[i], hi[i], lo[i + d], hi[i + d]);
                 } else {
-                    mul_add16(lo[i], hi[i], lo[i + d], hi[i + d], t);
+                    mul(lo[i], hi[i], lo[i + d], hi[i + d]);
                     lo[i + d] ^= lo[i];
                     hi[i + d] ^= hi[i];
                 }
@@ -225,7 +257,6 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N]
             if constexpr (J < NG) tc = tn;
         }
     });
-#endif
 }
 template <int N, class IdxF>
 __device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
