@@ -21,10 +21,12 @@
 // LDS (R rounds each way), so HBM sees only the data read, the optional Q0
 // copy and the parity write.
 //
-// Multiply by a constant c: y is split into 2-bit chunks (four per byte); each
-// chunk selects one of 4 bytes of a table dword with v_perm_b32(T, T, sel),
-// which needs a single SGPR, so the 16 table dwords of a constant stay in
-// SGPRs: 16 perms + 14 selector ops + 8 XOR3 per 4 symbols.
+// Multiply by a constant c: y is split into 3-bit chunks (bits 0-2, 3-5 and
+// the 2-bit 6-7 of each byte); a 3-bit chunk selects one of 8 table bytes
+// with v_perm_b32(src0 = SGPR dword, src1 = VGPR dword, sel), a 2-bit chunk
+// one of 4 with v_perm_b32(T, T, sel): 12 perms + 10 selector ops + 6 XOR3
+// per 4 symbols (mul_add16_c3; the 2-bit layout, -DCDA_RS16_CHUNK2, takes
+// 16 + 14 + 8).
 //
 // k > 512 (and arbitrary shard lengths in rsmt2d Codec.Encode) use the
 // LDS-staged log/exp kernel rs16_lds_kernel.
