@@ -191,8 +191,11 @@ constexpr int next_mul(int I) {
     return J;
 }
 
-template <int N, bool INV, bool ZERO_G0 = false, class IdxF>
-__device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
+// M independent register sets of N shards (pass B's residues) share every
+// butterfly constant: one table load and one VGPR copy per group serve all M.
+template <int N, bool INV, bool ZERO_G0 = false, int M = 1, class IdxF>
+__device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const Tab16& T,
+                                            IdxF idxf) {
     static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
     // The scalar loads are issued from inline asm: the compiler treats loads
@@ -208,9 +211,12 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N]
         constexpr int I = decltype(II)::value;
         constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
         if constexpr (!grp_mul<N, INV, ZERO_G0>(I)) {
-            sfor<g, g + d, 1>([&](auto ii) {      // multiply by zero: XOR only
-                lo[ii.value + d] ^= lo[ii.value];
-                hi[ii.value + d] ^= hi[ii.value];
+            sfor<0, M, 1>([&](auto mm) {
+                sfor<g, g + d, 1>([&](auto ii) {      // multiply by zero: XOR only
+                    constexpr int i = N * decltype(mm)::value + decltype(ii)::value;
+                    lo[i + d] ^= lo[i];
+                    hi[i + d] ^= hi[i];
+                });
             });
         } else {
             constexpr int J = next_mul<N, INV, ZERO_G0>(I);
@@ -223,7 +229,9 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N]
             if constexpr (J < NG) tn = load_tabs(tab_ptr(J));
             // the group's operands pass through volatile asm after the load, so
             // the scheduler cannot hoist the butterflies above it
-            launder<g, g + 2 * d>(lo, hi);
+            sfor<0, M, 1>([&](auto mm) {
+                launder<N * decltype(mm)::value + g, N * decltype(mm)::value + g + 2 * d>(lo, hi);
+            });
 #ifdef CDA_RS16_CHUNK2
             uint32_t t[16];
 #pragma unroll
@@ -244,17 +252,19 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[N], uint32_t (&hi)[N]
                 mul_add16_c3(xl, xh, yl, yh, t, bv);
 #endif
             };
-            sfor<g, g + d, 1>([&](auto ii) {
-                constexpr int i = decltype(ii)::value;
-                if constexpr (INV) {
-                    hi[i + d] ^= hi[i];
-                    lo[i + d] ^= lo[i];
-                    mul(lo[i], hi[i], lo[i + d], hi[i + d]);
-                } else {
-                    mul(lo[i], hi[i], lo[i + d], hi[i + d]);
-                    lo[i + d] ^= lo[i];
-                    hi[i + d] ^= hi[i];
-                }
+            sfor<0, M, 1>([&](auto mm) {
+                sfor<g, g + d, 1>([&](auto ii) {
+                    constexpr int i = N * decltype(mm)::value + decltype(ii)::value;
+                    if constexpr (INV) {
+                        hi[i + d] ^= hi[i];
+                        lo[i + d] ^= lo[i];
+                        mul(lo[i], hi[i], lo[i + d], hi[i + d]);
+                    } else {
+                        mul(lo[i], hi[i], lo[i + d], hi[i + d]);
+                        lo[i + d] ^= lo[i];
+                        hi[i + d] ^= hi[i];
+                    }
+                });
             });
             if constexpr (J < NG) tc = tn;
         }
@@ -367,14 +377,26 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     xchg_a_to_b();
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
     // residue R*wave + q: shards R*wave + q + S*t in registers R*t + q
-    sfor<0, R, 1>([&](auto qq) {
-        constexpr int q = decltype(qq)::value;
-        uint32_t l16[16], h16[16];
-        sfor<0, 16, 1>([&](auto tt) { l16[tt.value] = lo[R * tt.value + q]; h16[tt.value] = hi[R * tt.value + q]; });
-        ifft_regs<16>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
-        fft_regs<16, true>(l16, h16, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
-        sfor<0, 16, 1>([&](auto tt) { lo[R * tt.value + q] = l16[tt.value]; hi[R * tt.value + q] = h16[tt.value]; });
-    });
+    // all R residues go through each butterfly group together (same constants)
+    {
+        uint32_t lr[R * 16], hr[R * 16];
+        sfor<0, R, 1>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            sfor<0, 16, 1>([&](auto tt) {
+                lr[16 * q + tt.value] = lo[R * tt.value + q];
+                hr[16 * q + tt.value] = hi[R * tt.value + q];
+            });
+        });
+        layers_regs<16, true, false, R>(lr, hr, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
+        layers_regs<16, false, true, R>(lr, hr, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
+        sfor<0, R, 1>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            sfor<0, 16, 1>([&](auto tt) {
+                lo[R * tt.value + q] = lr[16 * q + tt.value];
+                hi[R * tt.value + q] = hr[16 * q + tt.value];
+            });
+        });
+    }
     xchg_b_to_a();
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
     fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); });
