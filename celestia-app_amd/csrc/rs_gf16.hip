@@ -87,8 +87,19 @@ __device__ __forceinline__ uint32_t perm2(uint32_t s0, uint32_t s1, uint32_t sel
 __device__ __forceinline__ void mul_add16_c3(uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh,
                                              const uint32_t (&t)[12], const uint32_t (&b)[8]) {
     const uint32_t m7 = 0x07070707u, m3 = 0x03030303u;
+#ifndef CDA_RS16_NO_SHIFT64
+    // one 64-bit shift serves both halves: the low dword's top bits take junk
+    // from yh, which the byte masks drop
+    const uint64_t y = (uint64_t)yl | ((uint64_t)yh << 32);
+    uint64_t y3, y6;
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(y3) : "v"(y));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(y6) : "v"(y));
+    const uint32_t c0 = yl & m7, c1 = (uint32_t)y3 & m7, c2 = (uint32_t)y6 & m3;
+    const uint32_t c3 = yh & m7, c4 = (uint32_t)(y3 >> 32) & m7, c5 = (uint32_t)(y6 >> 32) & m3;
+#else
     const uint32_t c0 = yl & m7, c1 = (yl >> 3) & m7, c2 = (yl >> 6) & m3;
     const uint32_t c3 = yh & m7, c4 = (yh >> 3) & m7, c5 = (yh >> 6) & m3;
+#endif
     xl = xor3(xl, perm2(t[0], b[0], c0), perm2(t[2], b[2], c1));
     xl = xor3(xl, perm1(t[8], c2), perm2(t[4], b[4], c3));
     xl = xor3(xl, perm2(t[6], b[6], c4), perm1(t[10], c5));
