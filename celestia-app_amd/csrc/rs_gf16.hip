@@ -164,25 +164,22 @@ __device__ __forceinline__ u32x16 sload16(const uint32_t* p) {
     asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
     return v;
 }
-__device__ __forceinline__ u32x8 sload8_at64(const uint32_t* p) {   // dwords 16..23
-    u32x8 v;
-    asm volatile("s_load_dwordx8 %0, %1, 0x40" : "=s"(v) : "s"(p) : "memory");
-    return v;
-}
-// one constant's tables: 16 dwords (+ 8 with the 3-bit layout)
+// (with 3-bit chunks only dwords 0..11 are used from SGPRs; the src1 halves,
+// dwords 12..19, are staged in LDS per workgroup and read as VGPRs)
 struct TabRegs {
     u32x16 a;
-#ifndef CDA_RS16_CHUNK2
-    u32x8 b;
-#endif
 };
 __device__ __forceinline__ TabRegs load_tabs(const uint32_t* p) {
     TabRegs r;
     r.a = sload16(p);
-#ifndef CDA_RS16_CHUNK2
-    r.b = sload8_at64(p);
-#endif
     return r;
+}
+struct TabB {   // src1 halves of one constant, [a][lo/hi] as 8 dwords
+    uint4 b0, b1;
+};
+__device__ __forceinline__ TabB load_tab_b(const uint32_t* TB, uint32_t idx) {
+    const uint4* p = reinterpret_cast<const uint4*>(TB + idx * 8);
+    return TabB{p[0], p[1]};
 }
 
 // Leopard skips the multiply when the skew is the modulus (log 0).  The FFT
@@ -206,7 +203,7 @@ constexpr int next_mul(int I) {
 // butterfly constant: one table load and one VGPR copy per group serve all M.
 template <int N, bool INV, bool ZERO_G0 = false, int M = 1, class IdxF>
 __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const Tab16& T,
-                                            IdxF idxf) {
+                                            const uint32_t* TB, IdxF idxf) {
     static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
     // The scalar loads are issued from inline asm: the compiler treats loads
@@ -216,8 +213,13 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
         return T.t + (size_t)idxf(grp_at<N, INV>(I, false), grp_at<N, INV>(I, true)) * kGf16TabWords;
     };
     constexpr int F0 = next_mul<N, INV, ZERO_G0>(-1);
+    auto tab_idx = [&](int I) { return idxf(grp_at<N, INV>(I, false), grp_at<N, INV>(I, true)); };
     TabRegs tc{};
     if constexpr (F0 < NG) tc = load_tabs(tab_ptr(F0));
+#ifndef CDA_RS16_CHUNK2
+    TabB bc{};
+    if constexpr (F0 < NG) bc = load_tab_b(TB, tab_idx(F0));
+#endif
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
         constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
@@ -231,13 +233,13 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
             });
         } else {
             constexpr int J = next_mul<N, INV, ZERO_G0>(I);
-#ifdef CDA_RS16_CHUNK2
             asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc.a)::"memory");   // this group's tables are here
-#else
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc.a), "+s"(tc.b)::"memory");
-#endif
             TabRegs tn;
             if constexpr (J < NG) tn = load_tabs(tab_ptr(J));
+#ifndef CDA_RS16_CHUNK2
+            TabB bn;
+            if constexpr (J < NG) bn = load_tab_b(TB, tab_idx(J));
+#endif
             // the group's operands pass through volatile asm after the load, so
             // the scheduler cannot hoist the butterflies above it
             sfor<0, M, 1>([&](auto mm) {
@@ -248,13 +250,10 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
 #pragma unroll
             for (int j = 0; j < 16; j++) t[j] = tc.a[j];
 #else
-            uint32_t t[12], bv[8];
+            uint32_t t[12];
 #pragma unroll
             for (int j = 0; j < 12; j++) t[j] = tc.a[j];
-#pragma unroll
-            for (int j = 0; j < 4; j++) asm volatile("v_mov_b32 %0, %1" : "=v"(bv[j]) : "s"(tc.a[12 + j]));
-#pragma unroll
-            for (int j = 0; j < 4; j++) asm volatile("v_mov_b32 %0, %1" : "=v"(bv[4 + j]) : "s"(tc.b[j]));
+            const uint32_t bv[8] = {bc.b0.x, bc.b0.y, bc.b0.z, bc.b0.w, bc.b1.x, bc.b1.y, bc.b1.z, bc.b1.w};
 #endif
             auto mul = [&](uint32_t& xl, uint32_t& xh, uint32_t yl, uint32_t yh) {
 #ifdef CDA_RS16_CHUNK2
@@ -277,20 +276,36 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
                     }
                 });
             });
-            if constexpr (J < NG) tc = tn;
+            if constexpr (J < NG) {
+                tc = tn;
+#ifndef CDA_RS16_CHUNK2
+                bc = bn;
+#endif
+            }
         }
     });
 }
 template <int N, class IdxF>
-__device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
-    layers_regs<N, true>(lo, hi, T, idxf);
+__device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
+                                          IdxF idxf) {
+    layers_regs<N, true>(lo, hi, T, TB, idxf);
 }
 template <int N, bool ZERO_G0 = false, class IdxF>
-__device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, IdxF idxf) {
-    layers_regs<N, false, ZERO_G0>(lo, hi, T, idxf);
+__device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
+                                         IdxF idxf) {
+    layers_regs<N, false, ZERO_G0>(lo, hi, T, TB, idxf);
 }
 
 constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
+// + the src1 table halves of the 2K-1 constants, 32 B each (K = 512: 160 KiB total)
+template <int K>
+constexpr uint32_t cw_lds_bytes() {
+#ifdef CDA_RS16_CHUNK2
+    return kXchgBytes;
+#else
+    return kXchgBytes + (2 * K - 1) * 32;
+#endif
+}
 
 template <int K>
 __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const RsJob job) {
@@ -298,6 +313,19 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
     const Tab16 T{tab};
+    const uint32_t* TB = X + kXchgBytes / 4;
+#ifndef CDA_RS16_CHUNK2
+    {   // stage dwords 12..19 of every constant's record (its src1 halves)
+        uint32_t* tb = X + kXchgBytes / 4;
+        for (uint32_t i = threadIdx.x; i < 2 * K - 1; i += 1024) {
+            const uint4* src = reinterpret_cast<const uint4*>(tab + (size_t)i * kGf16TabWords + 12);
+            uint4* dst = reinterpret_cast<uint4*>(tb + i * 8);
+            dst[0] = src[0];
+            dst[1] = src[1];
+        }
+        __syncthreads();
+    }
+#endif
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t off = 64 * (lane >> 3) + 4 * (lane & 7);    // lo dword; hi at +32
@@ -384,7 +412,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         asm volatile("" : "+s"(b));
         return b;
     };
-    ifft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); });
+    ifft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); });
     xchg_a_to_b();
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
     // residue R*wave + q: shards R*wave + q + S*t in registers R*t + q
@@ -398,8 +426,8 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
                 hr[16 * q + tt.value] = hi[R * tt.value + q];
             });
         });
-        layers_regs<16, true, false, R>(lr, hr, T, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
-        layers_regs<16, false, true, R>(lr, hr, T, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
+        layers_regs<16, true, false, R>(lr, hr, T, TB, [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
+        layers_regs<16, false, true, R>(lr, hr, T, TB, [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
             sfor<0, 16, 1>([&](auto tt) {
@@ -410,7 +438,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     }
     xchg_b_to_a();
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
-    fft_regs<S>(lo, hi, T, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); });
+    fft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); });
     sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
 }
 
@@ -510,11 +538,11 @@ hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s
     static bool attr = false;   // set once per instantiation (function attribute, all devices)
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs16_cw_kernel<K>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXchgBytes);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)cw_lds_bytes<K>());
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(rs16_cw_kernel<K>, dim3(ncw, n), dim3(1024), kXchgBytes, s, t.chunk, j);
+    hipLaunchKernelGGL(rs16_cw_kernel<K>, dim3(ncw, n), dim3(1024), cw_lds_bytes<K>(), s, t.chunk, j);
     return hipGetLastError();
 }
 
