@@ -79,7 +79,7 @@ __device__ __forceinline__ void mul_add16(uint32_t& xl, uint32_t& xh, uint32_t y
 // into chunks at bits 0-2, 3-5, 6-7 of each byte; a 3-bit chunk indexes 8
 // table bytes as v_perm(src0 = entries 4..7 in an SGPR, src1 = entries 0..3 in
 // a VGPR, sel) -- gfx9 VOP3 reads one SGPR, so the four src1 dword pairs are
-// copied to VGPRs once per butterfly group.  Per 4 symbols: 12 perms + 10
+// read from LDS (staged per workgroup) once per butterfly group.  Per 4 symbols: 12 perms + 10
 // selector ops + 6 XOR3 (2-bit layout: 16 + 14 + 8).
 __device__ __forceinline__ uint32_t perm2(uint32_t s0, uint32_t s1, uint32_t sel) {
     return __builtin_amdgcn_perm(s0, s1, sel);
