@@ -57,6 +57,122 @@ def rs_bytes(k: int) -> int:
     return 4 * k * k * SHARE                     # ODS read + 3 parity quadrants written
 
 
+# nominal 1 700 int32 VALU lane-ops per SHA-256 compression
+# (48 schedule steps x 12 + 64 rounds x 17 + 8, rounded up), deduplicated
+# compressions C(k) = 9*4k^2 + 3*4k(2k-1) + 2*4k + 2*(4k-1).  The peak is the
+# guide's 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T (SURVEY's 39.3 T
+# assumes 64 lanes per CU, half the guide's figure).
+ALG_LANE_OPS_PER_COMPRESSION = 1700
+
+
+def survey_compressions(k: int) -> int:
+    return 9 * 4 * k * k + 3 * 4 * k * (2 * k - 1) + 2 * 4 * k + 2 * (4 * k - 1)
+
+
+def combined_ceiling(k: int) -> float:
+    """SURVEY 8(d) 'Combined': squares/s per GPU = 1 / (B_RS / 8 TB/s +
+    C(k) * 1700 / 78.6 T), the serial sum of the RS HBM floor and the SHA-256
+    VALU floor."""
+    return 1.0 / (rs_bytes(k) / (PEAK_HBM_GBS * 1e9)
+                  + survey_compressions(k) * ALG_LANE_OPS_PER_COMPRESSION / (PEAK_VALU_TOPS * 1e12))
+
+
+def shard(rank: int, world: int, per_rank: int) -> range:
+    """Config 4 (BASELINE.json configs[3]): square indexes of
+    one rank.  Squares are independent, so rank g takes [g*B, (g+1)*B) --
+    with B = 128 and 8 ranks exactly the 1024 squares (seeds 0..1023) of the
+    config, no data-path collective."""
+    return range(rank * per_rank, (rank + 1) * per_rank)
+
+
+def time_region(step, steps: int, sync, world: int, reduce_max=None, barrier=None) -> float:
+    """The bench contract's timed region: barrier + sync, `steps` calls of
+    step(), sync + barrier, then the MAX of the elapsed time over ranks
+    (reduce_max(seconds) -> seconds; identity at world == 1)."""
+    if world > 1 and barrier:
+        barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1 and barrier:
+        barrier()
+    el = time.perf_counter() - t0
+    if world > 1 and reduce_max:
+        el = reduce_max(el)
+    return el
+
+
+def golden_config4():
+    """tests/golden/config4_k128.json (oracle digests of squares 0..127,
+    oracle/gen_config4.py), or None."""
+    p = os.path.join(ROOT, "tests", "golden", "config4_k128.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except OSError:
+        return None
+
+
+def golden_k512():
+    p = os.path.join(ROOT, "tests", "golden", "k512.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["squares"]
+    except (OSError, KeyError):
+        return None
+
+
+def host_buffer_rates(ctx, k: int, n: int = 16, reps: int = 3) -> dict:
+    """The drop-in boundary with host buffers: squares/s of
+    cda_extend_dah_batch when the ODS comes from and the EDS, roots and data
+    roots go back to host memory (PCIe inside, never the headline), and the
+    ProcessProposal latency from the block's host txs
+    (cda_construct_extend_dah: square construction + extension + DAH)."""
+    import numpy as np
+
+    from celestia_da import blobfactory, da, square as gsq, testfactory
+    ods = np.stack([testfactory.random_square(k, 5000 + i) for i in range(n)])
+    da.extend_dah_batch(ods, want_eds=True, ctx=ctx)             # warm-up (staging buffers)
+    t_full, t_roots = [], []
+    for _ in range(reps):
+        a = time.perf_counter()
+        da.extend_dah_batch(ods, want_eds=True, ctx=ctx)
+        t_full.append(time.perf_counter() - a)
+        a = time.perf_counter()
+        da.extend_dah_batch(ods, want_eds=False, ctx=ctx)
+        t_roots.append(time.perf_counter() - a)
+    full, roots = sorted(t_full)[reps // 2], sorted(t_roots)[reps // 2]
+    txs = blobfactory.full_block(1, 128)
+    gsq.construct_extend_dah(txs, 128, ctx=ctx)                  # warm-up
+    pp = []
+    for _ in range(5):
+        a = time.perf_counter()
+        gsq.construct_extend_dah(txs, 128, ctx=ctx)
+        pp.append(time.perf_counter() - a)
+    W = 2 * k
+    return {"k": k, "squares": n,
+            "eds_to_host_squares_per_s": n / full,
+            "eds_to_host_gb_per_s": n * (k * k + W * W) * SHARE / full / 1e9,
+            "roots_only_squares_per_s": n / roots,
+            "process_proposal_ms": 1e3 * sorted(pp)[2],
+            "note": "cda_extend_dah_batch from pageable numpy buffers: H2D ODS + D2H EDS/roots inside the time; "
+                    "process_proposal_ms = cda_construct_extend_dah on a full k=128 block of blob txs "
+                    "(host txs -> data root, roots back to the host)"}
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def stage_report(st: dict, k: int, batch: int, inplace: bool = False) -> dict:
     out = {}
     comp = compressions(k)
@@ -69,7 +185,8 @@ def stage_report(st: dict, k: int, batch: int, inplace: bool = False) -> dict:
             c = comp[name] * batch
             rec.update(bound="valu", achieved=c * SHA_SLOTS / (avg * 1e-3) / 1e12, peak=PEAK_VALU_TOPS,
                        unit="T issue-slots/s", achieved_instr=c * SHA_INSTR / (avg * 1e-3) / 1e12,
-                       compressions_per_s=c / (avg * 1e-3))
+                       compressions_per_s=c / (avg * 1e-3),
+                       frac_alg=c * ALG_LANE_OPS_PER_COMPRESSION / (avg * 1e-3) / (PEAK_VALU_TOPS * 1e12))
         elif name in ("rs_q0", "rs_q3"):
             # rs_q0: read ODS, write Q0|Q1|Q2 (4 k^2 shares); rs_q3: read Q2, write Q3 (2 k^2 shares)
             # (in place there is no Q0 copy: read Q0, write Q1|Q2 = 3 k^2 shares)
@@ -84,38 +201,74 @@ def stage_report(st: dict, k: int, batch: int, inplace: bool = False) -> dict:
     return out
 
 
-def load_traffic(stage: str):
-    """HBM bytes per launch of `stage` from the committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate
-    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), else None."""
+PMC_SUMMARY = os.environ.get("CDA_PMC_SUMMARY", "")
+
+
+def load_pmc(stage: str, field: str = "hbm_bytes_per_launch"):
+    """A per-launch figure of `stage` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from separate --pmc
+    passes of this bench: FETCH_SIZE / WRITE_SIZE -> HBM bytes, SQ_INSTS_VALU
+    ...), else None.  The newest summary is used unless CDA_PMC_SUMMARY names
+    one."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    files = [PMC_SUMMARY] if PMC_SUMMARY else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
+                                                     key=os.path.getmtime)
     if not files:
         return None
     try:
         with open(files[-1]) as f:
             d = json.load(f)
-        return d.get(stage, {}).get("hbm_bytes_per_launch")
+        return d.get(stage, {}).get(field)
     except Exception:
         return None
 
 
-def cpu_baseline(k: int, seconds: float, threads: int):
+def load_traffic(stage: str):
+    return load_pmc(stage, "hbm_bytes_per_launch")
+
+
+def cpu_threads(requested: int = 0) -> tuple:
+    """(threads used, host CPUs visible).  SURVEY 8(d) asks for all host
+    cores: every CPU in this process's affinity mask, capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box grants one
+    GPU's job 16 CPUs and sets OMP_NUM_THREADS=16; nproc there shows the
+    whole machine)."""
+    host = len(os.sched_getaffinity(0))
+    if requested:
+        return requested, host
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(host, cap) if cap > 0 else host), host
+
+
+def cpu_baseline(k: int, seconds: float, threads: int, runs: int = 5):
+    """CPU restatement (NOT the reference: Go is absent on both machines), timed
+    as SURVEY 8(d) asks: 1 warm-up, then `runs` samples of ~seconds/runs each,
+    the median squares/s reported."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
+    threads, host = cpu_threads(threads)
     ods = coracle.random_square(k, 0)
     coracle.cpu_baseline(ods, threads)          # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        coracle.cpu_baseline(ods, threads)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 1000:
-            break
-    return {"value": n / el, "unit": "squares/s", "cores": threads, "kind": "port",
-            "sample": f"{n} squares k={k} (oracle/cda_oracle.c oracle_cpu_baseline: rsmt2d structure, every "
-                      f"cell hashed in its row and its column tree, SHA-NI + AVX2 PSHUFB Leopard as in Go's "
-                      f"amd64 assembly; {threads} host threads, {el:.1f}s)"}
+    rates, total_n, total_t = [], 0, 0.0
+    for _ in range(runs):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            coracle.cpu_baseline(ods, threads)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / runs or n >= 1000:
+                break
+        rates.append(n / el)
+        total_n += n
+        total_t += el
+    rates.sort()
+    return {"value": rates[len(rates) // 2], "unit": "squares/s", "cores": threads, "kind": "port",
+            "label": "CPU restatement, not reference", "host_cpus": host, "cpu_model": cpu_model(),
+            "runs": rates,
+            "sample": f"median of {runs} runs, {total_n} squares k={k} in {total_t:.1f}s (oracle/cda_oracle.c "
+                      f"oracle_cpu_baseline: rsmt2d structure, every cell hashed in its row and its column tree, "
+                      f"SHA-NI + AVX2 PSHUFB Leopard as in Go's amd64 assembly; {threads} threads of {host} "
+                      f"visible CPUs, {cpu_model()})"}
 
 
 def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
@@ -398,14 +551,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--batch", type=int, default=128, help="squares per rank per step")
-    ap.add_argument("--distinct", type=int, default=8, help="distinct input squares per rank (tiled)")
+    ap.add_argument("--distinct", type=int, default=0,
+                    help="distinct input squares per rank, tiled to the batch (default: all distinct)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host CPUs (capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip k=512 and latency extras")
-    ap.add_argument("--layout", choices=("packed", "inplace"), default="packed",
-                    help="packed: ODS in its own k*k buffer (cda_extend_dah_device, Q0 copied into the EDS); "
-                         "inplace: ODS already in Q0 of the EDS (cda_extend_dah_inplace_device)")
+    ap.add_argument("--layout", choices=("packed", "inplace"), default="inplace",
+                    help="inplace: ODS already in Q0 of the EDS arena (cda_extend_dah_inplace_device, the layout "
+                         "rsmt2d's EDS has; no Q0 copy); packed: ODS in its own k*k buffer "
+                         "(cda_extend_dah_device, Q0 copied into the EDS)")
     args = ap.parse_args()
 
     import numpy as np
@@ -426,11 +581,14 @@ def main():
     W = 2 * k
     ctx = Context(local)
 
-    # inputs: distinct random squares per rank, tiled to the batch
-    nd = max(1, min(args.distinct, B))
-    base = np.stack([testfactory.random_square(k, rank * 100000 + i) for i in range(nd)])
-    ods_h = np.concatenate([base] * ((B + nd - 1) // nd))[:B]
+    # inputs: config 4's squares of this rank (seeds rank*B .. rank*B+B-1), all
+    # distinct unless --distinct asks for tiling
+    idx = list(shard(rank, world, B))
+    nd = B if args.distinct <= 0 else max(1, min(args.distinct, B))
+    base = np.stack([testfactory.random_square(k, i) for i in idx[:nd]])
+    ods_h = np.concatenate([base] * ((B + nd - 1) // nd))[:B] if nd < B else base
     d_ods = torch.from_numpy(np.ascontiguousarray(ods_h)).to(dev)
+    del base, ods_h
     d_eds = torch.empty(B * W * W * SHARE, dtype=torch.uint8, device=dev)
     d_rows = torch.empty(B * W * 90, dtype=torch.uint8, device=dev)
     d_cols = torch.empty(B * W * 90, dtype=torch.uint8, device=dev)
@@ -438,47 +596,52 @@ def main():
     d_status = torch.empty(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    if args.layout == "inplace":
-        # the ODS arrives in Q0 of the EDS arena (cda_extend_dah_inplace_device)
-        d_eds.view(B, W, W, SHARE)[:, :k, :k] = d_ods.view(B, k, k, SHARE)
-        del d_ods
+    def step_packed():
+        ctx.extend_dah_device(d_ods.data_ptr(), k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
+                              d_roots.data_ptr(), d_status.data_ptr(), stream)
 
-        def step():
-            ctx.extend_dah_inplace_device(k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
-                                          d_roots.data_ptr(), d_status.data_ptr(), stream)
+    def step_inplace():
+        ctx.extend_dah_inplace_device(k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
+                                      d_roots.data_ptr(), d_status.data_ptr(), stream)
+
+    if args.layout == "inplace":
+        # the ODS arrives in Q0 of the EDS arena; RS writes only Q1..Q3, so Q0
+        # stays intact across steps
+        d_eds.view(B, W, W, SHARE)[:, :k, :k] = d_ods.view(B, k, k, SHARE)
+        step = step_inplace
     else:
-        def step():
-            ctx.extend_dah_device(d_ods.data_ptr(), k, B, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
-                                  d_roots.data_ptr(), d_status.data_ptr(), stream)
+        step = step_packed
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    parity = {"checked": 0, "matched": 0}
     if not os.environ.get("CDA_BENCH_NOCHECK"):   # set only for timing-diagnostic library variants
         assert int(d_status.abs().sum().item()) == 0, "push-order status set on ordered input"
-        # tiled inputs must give tiled data roots
         roots = d_roots.view(B, 32).cpu().numpy()
-        for i in range(nd, B):
-            assert (roots[i] == roots[i % nd]).all()
+        if nd < B:   # tiled inputs must give tiled data roots
+            for i in range(nd, B):
+                assert (roots[i] == roots[i % nd]).all()
+        g = golden_config4()
+        if g and g.get("k") == k:
+            for j, i in enumerate(idx[:nd]):
+                want = g["squares"].get(str(i))
+                if want is not None:
+                    parity["checked"] += 1
+                    parity["matched"] += int(roots[j].tobytes().hex() == want["data_root"])
+            assert parity["matched"] == parity["checked"], f"data roots differ from the oracle fixture: {parity}"
 
     ctx.set_profiling(True)
     ctx.stage_times()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+
+    def reduce_max(x: float) -> float:
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    el = time_region(step, args.steps, lambda: torch.cuda.synchronize(dev), world, reduce_max, dist.barrier)
     ctx.set_profiling(False)
     st = ctx.stage_times()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
 
     total_sq = B * world * args.steps
     value = total_sq / el
@@ -488,16 +651,32 @@ def main():
     roofline = {"bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"], "unit": d["unit"],
                 "frac": d["frac"], "traffic": load_traffic(dom), "kernel": dom,
                 "achievable": d["achievable"], "frac_of_achievable": d["frac_of_achievable"]}
+    if "frac_alg" in d:
+        # SURVEY 8(d)'s own definition: compressions x 1700 nominal lane-ops
+        # against the 78.6 T VALU peak (frac above counts compiled issue slots)
+        roofline["frac_alg"] = d["frac_alg"]
+        roofline["achieved_alg_tops"] = d["frac_alg"] * PEAK_VALU_TOPS
+    ceiling = combined_ceiling(k)
+    roofline["combined_ceiling_squares_per_s"] = ceiling
+    roofline["combined_frac"] = (value / world) / ceiling
     rs_ms = sum(stages[s]["avg_ms"] for s in ("rs_q0", "rs_q3") if s in stages)
-    rs_roof = {"bound": "hbm", "achieved": rs_bytes(k) * B / (rs_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
-               "unit": "GB/s"}
+    rs_alg = rs_bytes(k) * B
+    rs_roof = {"bound": "hbm", "achieved": rs_alg / (rs_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+               "unit": "GB/s", "ms_per_step": rs_ms, "algorithmic_bytes_per_step": rs_alg}
     rs_roof["frac"] = rs_roof["achieved"] / rs_roof["peak"]
     rs_roof["achievable"] = ACHIEVABLE_HBM_GBS
-    # measured HBM bytes of the two RS launches of one step (PMC summary, the
-    # per-launch mean over rs_q0 and rs_q3), against rs_bytes(k) * B algorithmic
-    t_rs = load_traffic("rs_gf8_bs" if k == 128 else "rs_gf16")
+    # measured HBM bytes and VALU instructions of the two RS launches of one
+    # step (PMC summary: per-launch means over rs_q0 and rs_q3)
+    rs_stage = "rs_gf8_bs" if k == 128 else "rs_gf16"
+    t_rs = load_traffic(rs_stage)
     rs_roof["traffic"] = 2 * t_rs if t_rs else None
+    rs_roof["traffic_ratio"] = rs_roof["traffic"] / rs_alg if t_rs else None
     rs_roof["frac_of_achievable"] = rs_roof["achieved"] / ACHIEVABLE_HBM_GBS
+    v_rs = load_pmc(rs_stage, "SQ_INSTS_VALU")
+    if v_rs:
+        lane = 2 * v_rs * 64 / (rs_ms * 1e-3) / 1e12
+        rs_roof["valu"] = {"bound": "valu", "achieved": lane, "peak": PEAK_VALU_TOPS, "unit": "T lane-instr/s",
+                           "frac": lane / PEAK_VALU_TOPS, "source": "SQ_INSTS_VALU x 64 per step (PMC summary)"}
 
     extras = {}
     if rank == 0 and not args.no_extras:
@@ -511,6 +690,21 @@ def main():
             torch.cuda.synchronize(dev)
             lat.append(time.perf_counter() - a)
         extras["latency_single_square_ms"] = 1e3 * sorted(lat)[len(lat) // 2]
+        # the other device layout, same squares (a few steps, HIP-event stage times)
+        other = step_packed if args.layout == "inplace" else step_inplace
+        if args.layout == "inplace":
+            pass   # packed reads d_ods, still resident
+        else:
+            d_eds.view(B, W, W, SHARE)[:, :k, :k] = d_ods.view(B, k, k, SHARE)
+        other()
+        n_o = 5
+        el_o = time_region(other, n_o, lambda: torch.cuda.synchronize(dev), 1)
+        extras["layout_" + ("packed" if args.layout == "inplace" else "inplace")] = {
+            "squares_per_s": n_o * B / el_o, "ms_per_step": 1e3 * el_o / n_o}
+        try:
+            extras["host_buffers"] = host_buffer_rates(ctx, k)
+        except Exception as e:  # report, never lose the headline line
+            extras["host_buffers"] = {"error": f"{type(e).__name__}: {e}"}
         try:
             extras["square_construction"] = square_construction(ctx, dev, stream)
         except Exception as e:  # report, never lose the headline line
@@ -551,10 +745,25 @@ def main():
         torch.cuda.synchronize(dev)
         el5 = time.perf_counter() - a
         ctx.set_profiling(False)
+        st5 = stage_report(ctx.stage_times(), k5, 1)
         extras["k512"] = {"squares_per_s": n5 / el5, "ms_per_square": 1e3 * el5 / n5,
                           "ods_gb_per_s": n5 * k5 * k5 * SHARE / el5 / 1e9,
                           "data_root": g5.cpu().numpy().tobytes().hex(),
-                          "stages": stage_report(ctx.stage_times(), k5, 1)}
+                          "combined_ceiling_squares_per_s": combined_ceiling(k5),
+                          "combined_frac": (n5 / el5) / combined_ceiling(k5),
+                          "stages": st5}
+        gk = golden_k512()
+        if gk:
+            extras["k512"]["data_root_matches_oracle"] = extras["k512"]["data_root"] == gk["0"]["data_root"]
+        rs5 = sum(st5[s]["avg_ms"] for s in ("rs_q0", "rs_q3") if s in st5)
+        extras["k512"]["rs_roofline"] = {"bound": "hbm", "ms_per_square": rs5,
+                                         "achieved": rs_bytes(k5) / (rs5 * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+                                         "unit": "GB/s", "frac": rs_bytes(k5) / (rs5 * 1e-3) / 1e9 / PEAK_HBM_GBS}
+        v16 = load_pmc("rs_gf16", "SQ_INSTS_VALU")
+        if v16:
+            lane = 2 * v16 * 64 / (rs5 * 1e-3) / 1e12
+            extras["k512"]["rs_roofline"]["valu"] = {"achieved": lane, "peak": PEAK_VALU_TOPS,
+                                                     "unit": "T lane-instr/s", "frac": lane / PEAK_VALU_TOPS}
         # the same square twice per submission: the latency-bound tail (top
         # NMT levels, 12-level data-root chain) is shared by both squares
         del e5
@@ -606,11 +815,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8/u32",
-            "data": "synthetic random-namespace squares (testfactory mirror, SplitMix64)",
-            "config": {"workload": f"k={k} ODS batch: {B} squares per GPU per step "
-                                   f"(config 2 shape; x8 GPUs = config 4's 1024)",
-                       "k": k, "squares_per_gpu_per_step": B, "parallelism": f"dp{world} (independent squares)",
-                       "layout": args.layout},
+            "data": (f"synthetic random-namespace squares (testfactory mirror, SplitMix64), "
+                     f"{'all distinct' if nd == B else f'{nd} distinct tiled'}: square indexes "
+                     f"{idx[0]}..{idx[-1]} on rank 0"),
+            "config": {"workload": f"config 4 shard: {B} independent k={k} squares per GPU per step "
+                                   f"(rank g: squares [{B}g, {B}g+{B}); x8 GPUs = config 4's 1024)",
+                       "k": k, "squares_per_gpu_per_step": B, "distinct_squares": nd,
+                       "parallelism": f"dp{world} (independent squares)", "layout": args.layout},
+            "parity": {**parity, "fixture": "tests/golden/config4_k128.json (oracle data roots)"},
             "ods_gb_per_s": value * k * k * SHARE / 1e9,
             "roofline": roofline,
             "rs_roofline": rs_roof,

@@ -46,6 +46,7 @@ EXPORTED = (
     "cda_blob_commitments", "cda_blob_commitments_device",
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
+    "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -78,7 +79,7 @@ class SquareError(CdaError):
 
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()   # re-entrant: default_context() creates a Context (load()) under it
 
 
 def load():
@@ -141,6 +142,11 @@ def load():
         L.cda_repair.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
         L.cda_repair_device.argtypes = [ctxp, vp, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
         L.cda_rs_decode.argtypes = [ctxp, u8p, u8p, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.cda_nmt_axis_roots.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u32p, u8p, i32p]
+        L.cda_nmt_axis_root.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
+        L.cda_nmt_prove_range.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, u8p, u32p, u8p]
+        L.cda_merkle_root.argtypes = [ctxp, u8p, u64p, C.c_uint32, u8p]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L
@@ -234,8 +240,8 @@ _default = None
 
 def default_context() -> Context:
     global _default
-    with _lock:
-        pass
     if _default is None:
-        _default = Context(int(os.environ.get("CDA_DEVICE", "-1")))
+        with _lock:
+            if _default is None:
+                _default = Context(int(os.environ.get("CDA_DEVICE", "-1")))
     return _default

@@ -64,13 +64,23 @@ class DataAvailabilityHeader:
             self._hash = EMPTY_HASH
             return self._hash
         w = len(self.row_roots)
-        if len(self.column_roots) != w or any(len(r) != NMT_ROOT_SIZE for r in self.row_roots + self.column_roots):
-            raise ValueError("GPU data root needs equal counts of 90-byte roots")
         ctx = default_context()
-        rows = np.frombuffer(b"".join(self.row_roots), dtype=np.uint8).copy()
-        cols = np.frombuffer(b"".join(self.column_roots), dtype=np.uint8).copy()
         out = np.empty(32, dtype=np.uint8)
-        ctx.check(ctx.lib.cda_data_root(ctx.h, ptr(rows), ptr(cols), w, ptr(out)))
+        items = [bytes(r) for r in self.row_roots + self.column_roots]
+        if len(self.column_roots) == w and is_power_of_two(w) and all(len(r) == NMT_ROOT_SIZE for r in items):
+            # the DAH of a square: 2w 90-B roots (cda_data_root's fixed layout)
+            rows = np.frombuffer(b"".join(items[:w]), dtype=np.uint8).copy()
+            cols = np.frombuffer(b"".join(items[w:]), dtype=np.uint8).copy()
+            ctx.check(ctx.lib.cda_data_root(ctx.h, ptr(rows), ptr(cols), w, ptr(out)))
+        else:
+            # merkle.HashFromByteSlices over any slices (e.g. a header decoded
+            # from the wire with 6 rows, or roots of another size)
+            flat = np.frombuffer(b"".join(items) + b"\x00", dtype=np.uint8).copy()
+            off = np.zeros(len(items) + 1, dtype=np.uint64)
+            off[1:] = np.cumsum([len(x) for x in items])
+            import ctypes as C
+            ctx.check(ctx.lib.cda_merkle_root(ctx.h, ptr(flat), off.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                              len(items), ptr(out)))
         self._hash = out.tobytes()
         return self._hash
 

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstring>
 #include <new>
+#include <utility>
 
 #include "../../include/cda.h"
 #include "engine.h"
@@ -31,18 +32,74 @@ bool square_width(uint32_t n_shares, uint32_t* k) {
     return true;
 }
 
+// The last call's error text and push-order details, per calling thread.  The
+// context's own copy is overwritten by the next call on it (from any thread),
+// so cda_last_error / cda_push_order_detail read this snapshot instead.
+struct ThreadError {
+    std::string msg;
+    int32_t axis = -1;
+    uint32_t index = 0, pos = 0;
+};
+thread_local ThreadError tl_err;
+
+// A context may be driven from any OS thread (Go moves goroutines between
+// threads): its device becomes current for the call and the caller's device
+// is restored afterwards.
+struct DeviceScope {
+    int prev = -1, want;
+    explicit DeviceScope(int d) : want(d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~DeviceScope() {
+        if (prev >= 0 && prev != want) (void)hipSetDevice(prev);
+    }
+};
+
+// Lock the context, make its device current, order the call's GPU work after
+// the previous call's (Engine::order_begin / order_end on the stream the call
+// enqueues on: `stream`, or the context's private stream for host-buffer
+// calls), run f and publish the error to the calling thread.
+template <class F>
+int guarded_on(cda_ctx* ctx, const hipStream_t* stream, F&& f) {
+    if (!ctx) {
+        tl_err.msg = "null context";
+        return CDA_ERR_INVALID;
+    }
+    cda::Engine& e = ctx->eng;
+    std::lock_guard<std::mutex> g(e.mutex());
+    DeviceScope dev(e.device());
+    e.clear_error();
+    const hipStream_t s = stream ? *stream : e.stream();
+    int rc;
+    try {
+        e.order_begin(s);
+        rc = f(e);
+    } catch (const std::bad_alloc&) {
+        rc = e.fail(CDA_ERR_OOM, "host allocation failed");
+    } catch (...) {
+        rc = e.fail(CDA_ERR_DEVICE, "unexpected exception");
+    }
+    e.order_end(s);
+    tl_err.msg = e.last_error();
+    if (rc == CDA_ERR_PUSH_ORDER) {
+        tl_err.axis = e.po_axis;
+        tl_err.index = e.po_index;
+        tl_err.pos = e.po_pos;
+    }
+    return rc;
+}
+
 template <class F>
 int guarded(cda_ctx* ctx, F&& f) {
-    if (!ctx) return CDA_ERR_INVALID;
-    try {
-        std::lock_guard<std::mutex> g(ctx->eng.mutex());
-        ctx->eng.clear_error();
-        return f(ctx->eng);
-    } catch (const std::bad_alloc&) {
-        return ctx->eng.fail(CDA_ERR_OOM, "host allocation failed");
-    } catch (...) {
-        return ctx->eng.fail(CDA_ERR_DEVICE, "unexpected exception");
-    }
+    return guarded_on(ctx, nullptr, std::forward<F>(f));
+}
+
+// Device entry points enqueue on the caller's stream (NULL = HIP's default).
+template <class F>
+int guarded_stream(cda_ctx* ctx, void* stream, F&& f) {
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return guarded_on(ctx, &s, [&](cda::Engine& e) { return f(e, s); });
 }
 
 int not_pow2(cda::Engine& e, uint32_t n) {
@@ -50,9 +107,6 @@ int not_pow2(cda::Engine& e, uint32_t n) {
     snprintf(buf, sizeof buf, "number of shares is not a power of 2: got %u", n);
     return e.fail(CDA_ERR_NOT_POW2, buf);
 }
-
-// Last error of context-free calls (cda_square_layout with ctx == NULL).
-thread_local std::string tl_error;
 
 int plan_square(const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs, uint32_t max_square_size,
                 uint32_t threshold, int mode, cda::square::Plan* p, std::string* err) {
@@ -94,7 +148,10 @@ int cda_ctx_destroy(cda_ctx* ctx) {
     return CDA_OK;
 }
 
-const char* cda_last_error(cda_ctx* ctx) { return ctx ? ctx->eng.last_error().c_str() : tl_error.c_str(); }
+const char* cda_last_error(cda_ctx* ctx) {
+    (void)ctx;   // per calling thread: the message of this thread's last call (include/cda.h)
+    return tl_err.msg.c_str();
+}
 
 int cda_extend_shares(cda_ctx* ctx, const uint8_t* ods, uint32_t n_shares, uint8_t* eds) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
@@ -136,34 +193,30 @@ int cda_extend_dah_batch(cda_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t 
 
 int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t n, void* d_eds, void* d_row_roots,
                           void* d_col_roots, void* d_data_roots, int32_t* d_status, void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (k == 0 || (k & (k - 1))) return not_pow2(e, k * k);
         if (n == 0) return CDA_OK;
         if (!d_ods || !d_eds || !d_row_roots || !d_col_roots || !d_data_roots)
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        static thread_local cda::DevBuf err;   // per-thread err words (device)
-        hipError_t he = err.ensure((size_t)n * 4);
-        if (he != hipSuccess) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
+        uint32_t* err = e.err_words(n);
+        if (!err) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
         return e.enqueue_extend_dah(static_cast<const uint8_t*>(d_ods), k, n, static_cast<uint8_t*>(d_eds),
                                     static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
-                                    static_cast<uint8_t*>(d_data_roots), err.as<uint32_t>(), d_status, s);
+                                    static_cast<uint8_t*>(d_data_roots), err, d_status, s);
     });
 }
 
 int cda_extend_dah_inplace_device(cda_ctx* ctx, uint32_t k, uint32_t n, void* d_eds, void* d_row_roots,
                                   void* d_col_roots, void* d_data_roots, int32_t* d_status, void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (k == 0 || (k & (k - 1))) return not_pow2(e, k * k);
         if (n == 0) return CDA_OK;
         if (!d_eds || !d_row_roots || !d_col_roots || !d_data_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
-        static thread_local cda::DevBuf err;
-        hipError_t he = err.ensure((size_t)n * 4);
-        if (he != hipSuccess) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+        uint32_t* err = e.err_words(n);
+        if (!err) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
         return e.enqueue_extend_dah(nullptr, k, n, static_cast<uint8_t*>(d_eds), static_cast<uint8_t*>(d_row_roots),
-                                    static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_data_roots),
-                                    err.as<uint32_t>(), d_status, s);
+                                    static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_data_roots), err,
+                                    d_status, s);
     });
 }
 
@@ -194,17 +247,16 @@ int cda_data_root(cda_ctx* ctx, const uint8_t* row_roots, const uint8_t* col_roo
 
 int cda_push_order_detail(cda_ctx* ctx, int32_t* axis, uint32_t* index, uint32_t* position) {
     if (!ctx) return CDA_ERR_INVALID;
-    if (axis) *axis = ctx->eng.po_axis;
-    if (index) *index = ctx->eng.po_index;
-    if (position) *position = ctx->eng.po_pos;
+    if (axis) *axis = tl_err.axis;
+    if (index) *index = tl_err.index;
+    if (position) *position = tl_err.pos;
     return CDA_OK;
 }
 
 int cda_split_rows(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
                    void* d_row_block, uint32_t* d_err, void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (!d_ods_rows || !d_row_block || !d_err) return e.fail(CDA_ERR_INVALID, "null buffer");
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_split_rows(static_cast<const uint8_t*>(d_ods_rows), k, n_rows, row0,
                                     static_cast<uint8_t*>(d_row_block), d_err, s);
     });
@@ -212,10 +264,9 @@ int cda_split_rows(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_
 
 int cda_split_cols(cda_ctx* ctx, void* d_col_block, uint32_t k, uint32_t n_cols, uint32_t col0,
                    void* d_col_root_slots, void* d_row_subtree_slots, uint32_t* d_err, void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (!d_col_block || !d_col_root_slots || !d_row_subtree_slots || !d_err)
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_split_cols(static_cast<uint8_t*>(d_col_block), k, n_cols, col0,
                                     static_cast<uint8_t*>(d_col_root_slots), static_cast<uint8_t*>(d_row_subtree_slots),
                                     d_err, s);
@@ -225,10 +276,9 @@ int cda_split_cols(cda_ctx* ctx, void* d_col_block, uint32_t k, uint32_t n_cols,
 int cda_split_combine(cda_ctx* ctx, const void* d_row_subtree_slots, uint32_t parts, uint32_t k,
                       const void* d_col_root_slots, void* d_row_roots, void* d_col_roots, void* d_data_root,
                       void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (!d_row_subtree_slots || !d_col_root_slots || !d_row_roots || !d_col_roots || !d_data_root)
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_split_combine(static_cast<const uint8_t*>(d_row_subtree_slots), parts, k,
                                        static_cast<const uint8_t*>(d_col_root_slots),
                                        static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
@@ -263,11 +313,11 @@ int cda_square_layout(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, 
         return CDA_OK;
     };
     if (!ctx) {
-        tl_error.clear();
+        tl_err.msg.clear();
         try {
-            return run(&tl_error);
+            return run(&tl_err.msg);
         } catch (const std::bad_alloc&) {
-            tl_error = "host allocation failed";
+            tl_err.msg = "host allocation failed";
             return CDA_ERR_OOM;
         }
     }
@@ -325,7 +375,7 @@ int cda_square_construct_device(cda_ctx* ctx, const uint8_t* txs, const uint64_t
                                 const void* d_txs, uint32_t max_square_size, uint32_t threshold, int mode,
                                 void* d_ods, size_t ods_capacity, uint32_t* square_size, uint32_t* kept,
                                 uint32_t* n_kept, void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (!d_ods || !square_size || (n_txs && (!txs || !tx_off || !d_txs)))
             return e.fail(CDA_ERR_INVALID, "null buffer");
         cda::square::Plan p;
@@ -339,7 +389,6 @@ int cda_square_construct_device(cda_ctx* ctx, const uint8_t* txs, const uint64_t
         }
         if ((size_t)p.square_size * p.square_size * CDA_SHARE_SIZE > ods_capacity)
             return e.fail(CDA_ERR_INVALID, "ods capacity too small for the square");
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_square(p, static_cast<const uint8_t*>(d_txs), static_cast<uint8_t*>(d_ods), s);
     });
 }
@@ -361,7 +410,7 @@ int cda_blob_commitments(cda_ctx* ctx, const uint8_t* namespaces, const uint8_t*
 int cda_blob_commitments_device(cda_ctx* ctx, const uint8_t* namespaces, const uint64_t* data_off,
                                 const uint8_t* share_versions, uint32_t n, uint32_t threshold, const void* d_data,
                                 void* d_commitments, void* stream) {
-    return guarded(ctx, [&](cda::Engine& e) -> int {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
         if (n == 0) return CDA_OK;
         if (!namespaces || !data_off || !d_commitments || (data_off[n] > data_off[0] && !d_data))
             return e.fail(CDA_ERR_INVALID, "null buffer");
@@ -369,7 +418,6 @@ int cda_blob_commitments_device(cda_ctx* ctx, const uint8_t* namespaces, const u
         std::string err;
         if (cda::square::plan_commitments(namespaces, data_off, share_versions, n, threshold, &p, &err))
             return e.fail(CDA_ERR_SQUARE, err);
-        hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = default stream
         return e.enqueue_commitments(p, n, static_cast<const uint8_t*>(d_data), static_cast<uint8_t*>(d_commitments),
                                      s);
     });
@@ -396,6 +444,7 @@ int cda_square_create(cda_ctx* ctx, const uint8_t* ods, uint32_t n_shares, cda_s
 int cda_square_destroy(cda_square* sq) {
     if (!sq) return CDA_OK;
     std::lock_guard<std::mutex> g(sq->ctx->eng.mutex());
+    DeviceScope dev(sq->ctx->eng.device());
     delete sq;
     return CDA_OK;
 }
@@ -463,6 +512,61 @@ int cda_rs_decode(cda_ctx* ctx, uint8_t* shards, const uint8_t* present, uint32_
         if (n_codewords == 0) return CDA_OK;
         if (!shards || !present) return e.fail(CDA_ERR_INVALID, "null buffer");
         return e.host_rs_decode(shards, present, n_shards, shard_len, n_codewords);
+    });
+}
+
+int cda_nmt_axis_roots(cda_ctx* ctx, const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees,
+                       uint32_t square_size, const uint32_t* axis_index, uint8_t* roots, int32_t* status) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (n_trees == 0) return CDA_OK;
+        if (square_size == 0) return e.fail(CDA_ERR_INVALID, "cannot create a ErasuredNamespacedMerkleTree of squareSize == 0");
+        if (!roots || !axis_index || (n_cells && !cells)) return e.fail(CDA_ERR_INVALID, "null buffer");
+        if (cell_len < CDA_NAMESPACE_SIZE) return e.fail(CDA_ERR_INVALID, "data is too short to contain namespace ID");
+        for (uint32_t t = 0; t < n_trees; t++) {
+            // wrapper Push (pkg/wrapper/nmt_wrapper.go:94-96)
+            if ((uint64_t)axis_index[t] + 1 > 2ull * square_size || (uint64_t)n_cells > 2ull * square_size) {
+                char buf[160];
+                snprintf(buf, sizeof buf, "pushed past predetermined square size: boundary at %llu index at %u %u",
+                         2ull * square_size, axis_index[t], n_cells > 2 * square_size ? 2 * square_size : n_cells - 1);
+                return e.fail(CDA_ERR_INVALID, buf);
+            }
+        }
+        return e.nmt_axis_roots(cells, cell_len, n_cells, n_trees, square_size, axis_index, roots, status);
+    });
+}
+
+int cda_nmt_axis_root(cda_ctx* ctx, const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,
+                      uint32_t axis_index, uint8_t* root) {
+    return cda_nmt_axis_roots(ctx, cells, cell_len, n_cells, 1, square_size, &axis_index, root, nullptr);
+}
+
+int cda_nmt_prove_range(cda_ctx* ctx, const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,
+                        uint32_t axis_index, uint32_t start, uint32_t end, uint8_t* nodes, uint32_t* n_nodes,
+                        uint8_t* root) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (square_size == 0) return e.fail(CDA_ERR_INVALID, "cannot create a ErasuredNamespacedMerkleTree of squareSize == 0");
+        if (!cells || !n_nodes) return e.fail(CDA_ERR_INVALID, "null buffer");
+        if (cell_len < CDA_NAMESPACE_SIZE) return e.fail(CDA_ERR_INVALID, "data is too short to contain namespace ID");
+        if ((uint64_t)axis_index + 1 > 2ull * square_size || (uint64_t)n_cells > 2ull * square_size)
+            return e.fail(CDA_ERR_INVALID, "pushed past predetermined square size");
+        return e.nmt_prove_range(cells, cell_len, n_cells, square_size, axis_index, start, end, nodes, n_nodes, root);
+    });
+}
+
+int cda_merkle_root(cda_ctx* ctx, const uint8_t* items, const uint64_t* off, uint32_t n, uint8_t* out) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!out) return e.fail(CDA_ERR_INVALID, "null buffer");
+        if (n == 0) {   // merkle.HashFromByteSlices(nil) = sha256("")
+            static const uint8_t empty[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                                              0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                                              0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};
+            memcpy(out, empty, 32);
+            return CDA_OK;
+        }
+        if (!off || (off[n] > off[0] && !items)) return e.fail(CDA_ERR_INVALID, "null buffer");
+        for (uint32_t i = 0; i < n; i++)
+            if (off[i + 1] < off[i]) return e.fail(CDA_ERR_INVALID, "item offsets must be non-decreasing");
+        return e.merkle_root(items, off, n, out);
     });
 }
 

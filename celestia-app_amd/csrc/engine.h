@@ -66,6 +66,20 @@ class Engine {
     void clear_error() { err_.clear(); }
     int fail(int code, const std::string& msg) { err_ = msg; return code; }
     hipStream_t stream() const { return stream_; }
+    int device() const { return device_; }
+
+    // Scratch ordering.  The context's scratch buffers (leaf/level slots,
+    // digests, error words, staging) are shared by every call, and a device
+    // entry point only enqueues on the caller's stream.  Each call therefore
+    // starts with order_begin(s) -- s waits for the GPU work of the previous
+    // call, whatever stream it ran on -- and ends with order_end(s), which
+    // records that point.  The mutex orders the enqueues, the event orders the
+    // GPU work, so two calls on two streams never touch the scratch at once.
+    void order_begin(hipStream_t s);
+    void order_end(hipStream_t s);
+    // n push-order error words of a device entry point (context scratch), or
+    // NULL when the allocation fails.
+    uint32_t* err_words(uint32_t n) { return dev_err_.ensure((size_t)n * 4) == hipSuccess ? dev_err_.as<uint32_t>() : nullptr; }
 
     // Enqueue the full path for n squares of width k (device pointers).
     // d_err: n u32 words (min-encoded push-order violation, ~0 = ordered);
@@ -140,6 +154,14 @@ class Engine {
                const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index);
     int host_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t k, uint32_t shard_len, uint32_t n_codewords);
 
+    // Standalone erasured NMT trees and generic RFC-6962 roots (tree.hip).
+    int nmt_axis_roots(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees,
+                       uint32_t square_size, const uint32_t* axis, uint8_t* roots, int32_t* status);
+    int nmt_prove_range(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,
+                        uint32_t axis, uint32_t start, uint32_t end, uint8_t* nodes, uint32_t* n_nodes,
+                        uint8_t* root);
+    int merkle_root(const uint8_t* items, const uint64_t* off, uint32_t n, uint8_t* out);
+
     // Stage timing with HIP events on the launch stream (bench / profiling).
     enum Stage { kStageRsQ0 = 0, kStageRsQ3, kStageOrder, kStageLeaves, kStageLevels, kStageDataRoot, kNumStages };
     void set_profiling(bool on) { profiling_ = on; }
@@ -170,6 +192,8 @@ class Engine {
 
     int device_;
     hipStream_t stream_ = nullptr;
+    hipEvent_t order_ev_ = nullptr;   // end of the last call's GPU work
+    bool order_used_ = false;
     // Batch pipeline: RS of chunk i+1 (HBM/VALU mix) overlaps the SHA-256
     // stages of chunk i (VALU) on a second stream.
     hipStream_t rs_stream_ = nullptr, hash_stream_ = nullptr;
@@ -185,7 +209,7 @@ class Engine {
     DevBuf gf16_log_, gf16_exp_, gf16_skew_;
     DevBuf gf16_chunk_[2];   // k = 256, 512
     Gf16Dev gf16(uint32_t k) const;
-    DevBuf leaf_, lvl_, root_slots_, dig_, err_buf_;
+    DevBuf leaf_, lvl_, root_slots_, dig_, err_buf_, dev_err_;
     DevBuf h_ods_, h_eds_, h_rows_, h_cols_, h_roots_;   // device staging for host-buffer calls
     // square construction: device plan (segments + compact shares), device
     // copy of host txs, pinned staging for the plan and its copy-done event
@@ -198,7 +222,14 @@ class Engine {
     // repair: GF(2^8) tables (GF(2^16) ones are shared with the encoder),
     // codeword list, error locators, presence map, parity check scratch
     DevBuf gf8_log_, gf8_exp_, gf8_skew_, rp_cw_, rp_err_, rp_present_, rp_parity_, rp_buf_, rp_flags_;
-    std::vector<uint8_t> rp_roots_;   // roots of the last repair_verify (rows then columns)
+    std::vector<uint8_t> rp_roots_;
+    // standalone trees: host cells, all tree levels, axis indexes / error words, roots
+    DevBuf tr_cells_, tr_levels_, tr_axis_, tr_roots_;
+    DevBuf rs_pad_;   // Codec.Encode of a non-power-of-two shard count
+    int build_trees(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees, uint32_t square_size,
+                    const uint32_t* axis, std::vector<uint64_t>* level_off, std::vector<uint32_t>* err_out);
+    int tree_order_error(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,
+                         const uint32_t* axis, const std::vector<uint32_t>& err, int32_t* status);   // roots of the last repair_verify (rows then columns)
     int ensure_gf8_tables();
     int repair_verify(const uint8_t* d_eds, uint32_t k, const uint8_t* row_roots, const uint8_t* col_roots,
                       std::vector<uint8_t>& bad, hipStream_t s);

@@ -23,6 +23,10 @@ namespace cda {
 
 hipError_t DevBuf::ensure(size_t n) {
     if (n <= bytes && ptr) return hipSuccess;
+    // Growing: queued work (any stream) may still read the old buffer, so the
+    // device drains before it is freed.  Buffers only grow, so this happens a
+    // handful of times per context.
+    if (ptr) (void)hipDeviceSynchronize();
     release();
     size_t want = n < 256 ? 256 : n;
     hipError_t e = hipMalloc(&ptr, want);
@@ -46,10 +50,11 @@ Engine::Engine(int device) : device_(device) {}
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
     for (DevBuf* b : {&gf16_chunk_[0], &gf16_chunk_[1], &gf16_log_, &gf16_exp_,
-                      &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &h_ods_, &h_eds_,
+                      &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &dev_err_, &h_ods_, &h_eds_,
                       &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_, &cm_plan_, &cm_tables_,
                       &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_, &gf8_log_, &gf8_exp_, &gf8_skew_, &rp_cw_,
-                      &rp_err_, &rp_present_, &rp_parity_, &rp_buf_, &rp_flags_})
+                      &rp_err_, &rp_present_, &rp_parity_, &rp_buf_, &rp_flags_, &tr_cells_, &tr_levels_,
+                      &tr_axis_, &tr_roots_, &rs_pad_})
         b->release();
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);
@@ -59,6 +64,7 @@ Engine::~Engine() {
     }
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     for (hipEvent_t e : sync_events_) (void)hipEventDestroy(e);
+    if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (rs_stream_) (void)hipStreamDestroy(rs_stream_);
     if (hash_stream_) (void)hipStreamDestroy(hash_stream_);
@@ -82,6 +88,7 @@ int Engine::init() {
     int rc;
     if ((rc = check(hipSetDevice(device_), "hipSetDevice"))) return rc;
     if ((rc = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if ((rc = check(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority), so RS workgroups win free CU slots.
     // CDA_RS_CU=S:R[:G] (tuning): spatial split of the pipeline's streams.  CU
@@ -184,6 +191,14 @@ Gf16Dev Engine::gf16(uint32_t k) const {
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+void Engine::order_begin(hipStream_t s) {
+    if (order_used_) (void)hipStreamWaitEvent(s, order_ev_, 0);
+}
+
+void Engine::order_end(hipStream_t s) {
+    if (order_ev_ && hipEventRecord(order_ev_, s) == hipSuccess) order_used_ = true;
+}
 
 hipEvent_t Engine::take_event() {
     if (!event_pool_.empty()) {
@@ -453,11 +468,30 @@ int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uin
         snprintf(buf, sizeof buf, "chunkSize %u must be a multiple of 64 bytes", len);
         return fail(CDA_ERR_CHUNK_SIZE, buf);
     }
-    if (!pow2(k)) return fail(CDA_ERR_UNSUPPORTED, "shard count must be a power of two");
+    if (k == 0) return fail(CDA_ERR_UNSUPPORTED, "no shards");
+    if (k > 1024) return fail(CDA_ERR_UNSUPPORTED, "more than 2048 shards");
+    if (!pow2(k)) {
+        // klauspost leopardFF8/16 encode with dataShards = parityShards = k:
+        // m = ceilPow2(k); the IFFT reads k data shards and zeros up to m
+        // (ifftDITEncoder's mtrunc), the FFT's first k outputs are the parity.
+        // Same result: encode the zero-padded m-shard codeword, keep k shards.
+        uint32_t m = 1;
+        while (m < k) m <<= 1;
+        const size_t in_cw = (size_t)k * len, pad_cw = (size_t)m * len;
+        int rc;
+        if ((rc = check(rs_pad_.ensure(2 * pad_cw * n), "hipMalloc rs padding"))) return rc;
+        uint8_t* pad_in = rs_pad_.as<uint8_t>();
+        uint8_t* pad_out = pad_in + pad_cw * n;
+        if ((rc = check(hipMemsetAsync(pad_in, 0, pad_cw * n, s), "hipMemsetAsync"))) return rc;
+        if ((rc = check(hipMemcpy2DAsync(pad_in, pad_cw, d_data, in_cw, in_cw, n, hipMemcpyDeviceToDevice, s),
+                        "copy")))
+            return rc;
+        if ((rc = enqueue_rs(pad_in, pad_out, m, len, n, s))) return rc;
+        return check(hipMemcpy2DAsync(d_parity, in_cw, pad_out, pad_cw, in_cw, n, hipMemcpyDeviceToDevice, s), "copy");
+    }
     if (k == 1)
         return check(hipMemcpyAsync(d_parity, d_data, (size_t)len * n, hipMemcpyDeviceToDevice, s), "copy");
     if (k <= 128) return check(launch_rs8_flat(d_data, d_parity, k, len, n, s), "rs8 flat");
-    if (k > 1024) return fail(CDA_ERR_UNSUPPORTED, "more than 2048 shards");
     return check(launch_rs16_flat(gf16(k), d_data, d_parity, k, len, n, s), "rs16 flat");
 }
 

@@ -36,6 +36,11 @@
  *   cda_square_*           resident squares: proof.NewShareInclusionProofFromEDS
  *                          (pkg/proof/proof.go:77), inclusion.GetCommitment
  *                          (pkg/inclusion/get_commit.go:12)
+ *   cda_nmt_axis_root(s) / cda_nmt_prove_range
+ *                          wrapper.NewErasuredNamespacedMerkleTree + Push +
+ *                          Root / ProveRange (pkg/wrapper/nmt_wrapper.go:55-129)
+ *   cda_merkle_root        go-square/merkle HashFromByteSlices (DAH.Hash for
+ *                          any root count, data_availability_header.go:92-108)
  *
  * Conventions
  *   - All buffers are plain byte arrays; shares are row-major and contiguous
@@ -44,12 +49,16 @@
  *   - Inputs are borrowed for the duration of the call; outputs are written to
  *     caller-owned buffers; the library keeps no pointer after return.
  *   - Return value: CDA_OK (0) or a negative CDA_ERR_* code.  The message of
- *     the last error on a context is available from cda_last_error(); it uses
- *     the reference's error text where one exists.  The library never aborts
- *     across the ABI.
+ *     the calling thread's last call is available from cda_last_error(); it
+ *     uses the reference's error text where one exists.  The library never
+ *     aborts across the ABI.
  *   - A context owns one HIP device and stream; calls on one context are
  *     serialised by an internal mutex (rsmt2d calls Codec/Tree from many
- *     goroutines).  Use one context per device.
+ *     goroutines) and may come from any OS thread (the context's device is
+ *     made current for the call).  Device entry points only enqueue on the
+ *     caller's stream; their GPU work is ordered after the previous call's on
+ *     the same context (any stream), because the context's scratch is shared.
+ *     Use one context per device.
  */
 #ifndef CDA_H
 #define CDA_H
@@ -86,7 +95,10 @@ typedef struct cda_ctx cda_ctx;
 /* Context lifecycle. device: HIP ordinal (-1 = current device). */
 int cda_ctx_create(int device, cda_ctx **out);
 int cda_ctx_destroy(cda_ctx *ctx);
-/* Message of the last failed call on ctx (never NULL; "" after success). */
+/* Message of the calling thread's last call (never NULL; "" after success).
+ * Thread-local, so a concurrent call on the same context from another thread
+ * cannot change or free it; a cgo caller reads it in the same C call or under
+ * runtime.LockOSThread. */
 const char *cda_last_error(cda_ctx *ctx);
 /* Library version string, e.g. "cda 0.1.0 gfx950". */
 const char *cda_version(void);
@@ -142,8 +154,8 @@ int cda_rs_encode(cda_ctx *ctx, const uint8_t *data, uint32_t n_shards, uint32_t
  * (w roots of 90 bytes each). w == 0 gives sha256("") like Hash() on a nil DAH. */
 int cda_data_root(cda_ctx *ctx, const uint8_t *row_roots, const uint8_t *col_roots, uint32_t w, uint8_t *data_root);
 
-/* Details of the last CDA_ERR_PUSH_ORDER on ctx: axis (0 row, 1 column), the
- * axis index, and the leaf position whose push failed. */
+/* Details of the calling thread's last CDA_ERR_PUSH_ORDER: axis (0 row, 1
+ * column), the axis index, and the leaf position whose push failed. */
 int cda_push_order_detail(cda_ctx *ctx, int32_t *axis, uint32_t *index, uint32_t *position);
 
 /* Config 5: ONE square split across G ranks (one GPU each), row blocks +
@@ -298,6 +310,40 @@ int cda_repair_device(cda_ctx *ctx, void *d_eds, const uint8_t *present, uint32_
  * and parity).  Fewer than n_shards present: CDA_ERR_UNREPAIRABLE. */
 int cda_rs_decode(cda_ctx *ctx, uint8_t *shards, const uint8_t *present, uint32_t n_shards, uint32_t shard_len,
                   uint32_t n_codewords);
+
+/* ---- Standalone erasured NMT trees -----------
+ * wrapper.NewErasuredNamespacedMerkleTree(squareSize, axisIndex), n_cells
+ * Pushes and Root() (pkg/wrapper/nmt_wrapper.go:55-124) for trees built
+ * outside ComputeExtendedDataSquare (pkg/proof/proof.go:157-189,
+ * pkg/inclusion/nmt_caching.go:96-109, test/util/malicious/tree.go:46-70).
+ *   cells: n_trees * n_cells * cell_len bytes; push i of tree t at
+ *     (t*n_cells + i)*cell_len; cell_len >= 29 (NamespaceSize).  The leaf
+ *     namespace is cell[0:29] when i < square_size and axis_index[t] <
+ *     square_size (isQuadrantZero, :138-140), else ParitySharesNamespace.
+ *   n_cells: any count <= 2*square_size (nmt's RFC-6962 split for non powers
+ *     of two); 0 gives NmtHasher.EmptyRoot.
+ *   roots: n_trees * 90 bytes; status (n_trees int32, may be NULL): CDA_OK or
+ *     CDA_ERR_PUSH_ORDER per tree (nmt Push ErrInvalidPushOrder; the call then
+ *     returns CDA_ERR_PUSH_ORDER with the first tree's message).
+ * 512-byte cells, a power-of-two n_cells and consecutive axis indexes (rows
+ * of a square) run on the square kernels; anything else on generic ones. */
+int cda_nmt_axis_roots(cda_ctx *ctx, const uint8_t *cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees,
+                       uint32_t square_size, const uint32_t *axis_index, uint8_t *roots, int32_t *status);
+int cda_nmt_axis_root(cda_ctx *ctx, const uint8_t *cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,
+                      uint32_t axis_index, uint8_t *root);
+/* (*ErasuredNamespacedMerkleTree).ProveRange(start, end) (:126-129 -> nmt
+ * ProveRange) of the tree above: nodes receives the proof nodes (90 B each, the
+ * maximal subtrees outside [start, end) depth first, left to right; at most
+ * 2*ceil(log2 n_cells)), *n_nodes their count, root (may be NULL) the root.
+ * start >= end or end > n_cells: CDA_ERR_INVALID ("invalid proof range"). */
+int cda_nmt_prove_range(cda_ctx *ctx, const uint8_t *cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,
+                        uint32_t axis_index, uint32_t start, uint32_t end, uint8_t *nodes, uint32_t *n_nodes,
+                        uint8_t *root);
+/* go-square/merkle HashFromByteSlices (RFC-6962) over n byte slices, item i =
+ * items[off[i] .. off[i+1]) (off has n + 1 entries): (*DataAvailabilityHeader)
+ * .Hash for any root count and size (data_availability_header.go:92-108).
+ * n == 0 gives sha256(""). */
+int cda_merkle_root(cda_ctx *ctx, const uint8_t *items, const uint64_t *off, uint32_t n, uint8_t out[32]);
 
 /* Stage timing (HIP events on the launch stream).  When enabled, every
  * enqueued stage is bracketed by events; cda_stage_times synchronises them and

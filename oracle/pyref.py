@@ -173,6 +173,16 @@ def leopard_encode(data: np.ndarray) -> np.ndarray:
         raise ValueError(f"chunkSize {L} must be a multiple of 64 bytes")
     if k == 1:
         return data.copy()
+    if k & (k - 1):
+        # klauspost leopardFF8/16 encode with dataShards == parityShards == k
+        # (rsmt2d LeoRSCodec.Encode of a non-power-of-two shard count, e.g.
+        # pkg/wrapper/nmt_wrapper_test.go:152-180): m = ceilPow2(k), the IFFT
+        # reads the k data shards and zeros up to m (ifftDITEncoder's mtrunc),
+        # the first k FFT outputs are the parity.
+        m = 1 << (k - 1).bit_length()
+        pad = np.zeros((m, L), dtype=np.uint8)
+        pad[:k] = data
+        return leopard_encode(pad)[:k]
     F = field_for(k)
     if F.bits == 8:
         out = _encode_symbols(F, data.astype(np.int64))

@@ -1,0 +1,139 @@
+"""Config 4 (BASELINE.json configs[3]): a batch of independent k=128 squares
+sharded across GPUs with no collective.
+
+  * GPU: one rank's whole shard -- 128 distinct squares (indexes 0..127, the
+    squares GPU 0 of an 8-GPU node processes) in ONE device submission, every
+    data root and every square's row/column roots checked against the oracle
+    fixture tests/golden/config4_k128.json (oracle/gen_config4.py), a sample
+    of full EDSs by digest and one square byte-for-byte against the C oracle.
+    Reference analogue: the block replay of app/process_proposal.go:138-152.
+  * CPU (gloo, world size 2): bench.py's rank partition and the MAX-over-ranks
+    reduction of its timed region.
+"""
+import hashlib
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _fixture():
+    with open(os.path.join(HERE, "golden", "config4_k128.json")) as f:
+        return json.load(f)
+
+
+def _sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_fixture_covers_rank0_shard():
+    import bench
+    g = _fixture()
+    assert g["k"] == 128 and len(g["squares"]) == 128
+    assert [str(i) for i in bench.shard(0, 8, 128)] == sorted(g["squares"], key=int)
+
+
+def test_shard_partitions_config4():
+    import bench
+    for world in (1, 2, 4, 8):
+        per = 1024 // world
+        seen = [i for r in range(world) for i in bench.shard(r, world, per)]
+        assert seen == list(range(1024))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["inplace", "packed"])
+def test_config4_rank_shard_on_gpu(ctx, layout):
+    import torch
+
+    import coracle
+    from celestia_da import testfactory
+    g = _fixture()
+    k, n = 128, 128
+    W = 2 * k
+    dev = torch.device("cuda", 0)
+    ods = np.stack([testfactory.random_square(k, i) for i in range(n)])
+    d_ods = torch.from_numpy(ods).to(dev)
+    eds = torch.zeros(n, W * W * 512, dtype=torch.uint8, device=dev)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    if layout == "inplace":
+        eds.view(n, W, W, 512)[:, :k, :k] = d_ods.view(n, k, k, 512)
+        ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                      status.data_ptr(), stream)
+    else:
+        ctx.extend_dah_device(d_ods.data_ptr(), k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(),
+                              roots.data_ptr(), status.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    r, c, dr = rows.cpu().numpy(), cols.cpu().numpy(), roots.cpu().numpy()
+    for i in range(n):
+        want = g["squares"][str(i)]
+        assert _sha(ods[i]) == want["ods_sha256"], i
+        assert dr[i].tobytes().hex() == want["data_root"], i
+        assert _sha(r[i].reshape(W, 90)) == want["row_roots_sha256"], i
+        assert _sha(c[i].reshape(W, 90)) == want["col_roots_sha256"], i
+    for i in (0, 1, 63, 64, 126, 127):
+        assert _sha(eds[i].cpu().numpy()) == g["squares"][str(i)]["eds_sha256"], i
+    e_eds, e_rows, e_cols, e_root = coracle.cpu_baseline(ods[77], 8)
+    assert np.array_equal(eds[77].cpu().numpy().reshape(-1, 512), e_eds)
+    assert np.array_equal(r[77].reshape(W, 90), e_rows) and np.array_equal(c[77].reshape(W, 90), e_cols)
+    assert dr[77].tobytes() == e_root
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench_worker(rank, world, port, q):
+    import time
+
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def reduce_max(x):
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    steps, dt = 4, 0.05 * (rank + 1)          # rank 1 is the slow one
+    el = bench.time_region(lambda: time.sleep(dt), steps, lambda: None, world, reduce_max, dist.barrier)
+    q.put((rank, el, list(bench.shard(rank, world, 1024 // world))))
+    dist.destroy_process_group()
+
+
+def test_bench_rank_partition_and_max_time_gloo():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, el0, s0), (_, el1, s1) = msgs
+    assert el0 == el1, "every rank must report the same (max) time"
+    assert el0 >= 4 * 0.1 - 1e-3, "the max over ranks is the slow rank's time"
+    assert s0 == list(range(512)) and s1 == list(range(512, 1024))

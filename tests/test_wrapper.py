@@ -89,3 +89,114 @@ def test_compute_extended_data_square(ctx):
     rows = eds.row_roots()
     assert len(rows) == 2 * k
     assert rows[0] == pyref.axis_root(eds.row(0), k, 0)
+
+
+# ---- standalone trees on the GPU (cda_nmt_axis_root / cda_nmt_prove_range) ----
+import proofs  # noqa: E402  (oracle: nmt ProveRange / VerifyInclusion restatement)
+from celestia_da import testfactory  # noqa: E402
+
+
+def gpu_erasured_data(ctx, k, seed=1):
+    """generateErasuredData (:139-152) with the GPU codec: k random namespaced
+    shares (GenerateRandNamespacedRawData, sorted) + LeoRSCodec.Encode."""
+    from celestia_da import rsmt2d
+    raw = testfactory.random_namespaced_shares(k, 500 + seed)
+    parity = rsmt2d.LeoRSCodec(ctx).encode(raw)
+    assert np.array_equal(parity, pyref.leopard_encode(raw)), "codec parity differs from the oracle"
+    return [bytes(s) for s in raw] + [bytes(p) for p in parity]
+
+
+@pytest.mark.gpu
+def test_root_erasured_tree_on_gpu(ctx):
+    """TestRootErasuredNamespacedMerkleTree (:49-73): 8 pushes into a k=8 tree;
+    the GPU root equals the oracle's erasured root and differs from a plain
+    NMT root of the same data."""
+    size = 8
+    data = [bytes(s) for s in testfactory.random_namespaced_shares(size, 77)]
+    tree = wrapper.new_erasured_namespaced_merkle_tree(size, 0, ctx)
+    for d in data:
+        tree.push(d)
+    root = tree.root()
+    assert root == pyref.nmt_root_from_nodes(pyref.erasured_leaves(data, size, 0))
+    assert root != pyref.nmt_root_from_nodes([pyref.nmt_hash_leaf(d) for d in data])   # nmtStandard.Push(d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(1, 17))
+def test_prove_range_on_gpu(ctx, k):
+    """TestErasuredNamespacedMerkleTree_ProveRange (:152-180), squareSize 1..16
+    (non-powers of two included: nmt's RFC-6962 split, Leopard's padded
+    encode): every single-leaf proof equals the oracle's nodes and verifies
+    against the root with the leaf's namespace (parity namespace in the
+    parity half)."""
+    data = gpu_erasured_data(ctx, k, seed=k)
+    tree = wrapper.new_erasured_namespaced_merkle_tree(k, 0, ctx)
+    for d in data:
+        tree.push(d)
+    leaves = pyref.erasured_leaves(data, k, 0)
+    root = tree.root()
+    assert root == pyref.nmt_root_from_nodes(leaves)
+    for i in range(len(data)):
+        nodes = tree.prove_range(i, i + 1)
+        assert nodes, "proof must not be empty"
+        assert nodes == proofs.nmt_range_proof(leaves, i, i + 1)
+        ns = data[i][:29] if i < k else wrapper.PARITY_SHARES_NAMESPACE
+        assert proofs.nmt_verify_range(root, nodes, i, i + 1, len(data), [pyref.nmt_hash_leaf(ns + data[i])])
+    with pytest.raises(Exception, match="invalid proof range"):
+        tree.prove_range(3, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n_cells,cell_len,axes", [
+    (8, 16, 512, [0, 1, 2, 3]),          # rows of a square: fast path
+    (8, 16, 512, [9, 3, 12]),            # scattered axes: generic kernels
+    (8, 11, 512, [0, 8]),                # ragged leaf count
+    (4, 8, 64, [1, 2]),                  # 64-B chunks (rsmt2d chunk size)
+    (128, 256, 512, list(range(64, 192))),   # pkg/inclusion/nmt_caching.go: many rows at once
+])
+def test_axis_roots_batch_on_gpu(ctx, k, n_cells, cell_len, axes):
+    rng = np.random.default_rng(k * 1000 + n_cells)
+    cells = rng.integers(0, 256, (len(axes), n_cells, cell_len), dtype=np.uint8)
+    cells[:, :, :29] = 0
+    cells[:, :, 28] = np.arange(n_cells, dtype=np.uint8)[None, :]   # ordered namespaces
+    roots = wrapper.axis_roots(cells, k, axes, ctx)
+    for t, ax in enumerate(axes):
+        assert roots[t].tobytes() == pyref.axis_root(list(cells[t]), k, ax), (t, ax)
+
+
+@pytest.mark.gpu
+def test_axis_roots_push_order_on_gpu(ctx):
+    from celestia_da import PushOrderError
+    k = 8
+    cells = np.zeros((2, 16, 512), dtype=np.uint8)
+    cells[:, :, 28] = np.arange(16, dtype=np.uint8)[None, :]
+    cells[1, 5, 28], cells[1, 6, 28] = 6, 5
+    with pytest.raises(PushOrderError, match="lexicographically ordered"):
+        wrapper.axis_roots(cells, k, [0, 1], ctx)
+    axis, idx, pos = ctx.push_order_detail()
+    assert (idx, pos) == (1, 6)
+
+
+@pytest.mark.gpu
+def test_seeded_tree_recomputes_when_fed_other_cells(ctx):
+    """A tree seeded with the square's GPU root returns it only for the cells
+    it was seeded for; pushing changed cells gives the root of what was
+    pushed (not a stale seed)."""
+    from celestia_da import da
+    k = 4
+    ods = testfactory.random_square(k, 3)
+    eds = da.extend_shares(ods)
+    seeded_root = eds.row_roots()[1]
+    row = eds.row(1)
+    same = wrapper.new_erasured_namespaced_merkle_tree(k, 1, ctx)
+    same.seed(seeded_root, [np.frombuffer(c, dtype=np.uint8) for c in row])
+    for c in row:
+        same.push(c)
+    assert same.root() == seeded_root
+    changed = list(row)
+    changed[k + 1] = bytes(512)            # a parity cell altered after extension
+    t = wrapper.new_erasured_namespaced_merkle_tree(k, 1, ctx)
+    t.seed(seeded_root, [np.frombuffer(c, dtype=np.uint8) for c in row])
+    for c in changed:
+        t.push(c)
+    assert t.root() == pyref.axis_root(changed, k, 1) != seeded_root
