@@ -124,42 +124,58 @@ def golden_k512():
         return None
 
 
-def host_buffer_rates(ctx, k: int, n: int = 16, reps: int = 3) -> dict:
+def host_buffer_rates(ctx, k: int, n: int = 16, reps: int = 5) -> dict:
     """The drop-in boundary with host buffers: squares/s of
     cda_extend_dah_batch when the ODS comes from and the EDS, roots and data
     roots go back to host memory (PCIe inside, never the headline), and the
     ProcessProposal latency from the block's host txs
-    (cda_construct_extend_dah: square construction + extension + DAH)."""
+    (cda_construct_extend_dah: square construction + extension + DAH).
+    Host buffers are allocated once and reused, as a node reuses them (fresh
+    pages would add the kernel's first-touch faults to every call)."""
+    import ctypes as C
+
     import numpy as np
 
-    from celestia_da import blobfactory, da, square as gsq, testfactory
-    ods = np.stack([testfactory.random_square(k, 5000 + i) for i in range(n)])
-    da.extend_dah_batch(ods, want_eds=True, ctx=ctx)             # warm-up (staging buffers)
-    t_full, t_roots = [], []
-    for _ in range(reps):
-        a = time.perf_counter()
-        da.extend_dah_batch(ods, want_eds=True, ctx=ctx)
-        t_full.append(time.perf_counter() - a)
-        a = time.perf_counter()
-        da.extend_dah_batch(ods, want_eds=False, ctx=ctx)
-        t_roots.append(time.perf_counter() - a)
-    full, roots = sorted(t_full)[reps // 2], sorted(t_roots)[reps // 2]
-    txs = blobfactory.full_block(1, 128)
-    gsq.construct_extend_dah(txs, 128, ctx=ctx)                  # warm-up
-    pp = []
-    for _ in range(5):
-        a = time.perf_counter()
-        gsq.construct_extend_dah(txs, 128, ctx=ctx)
-        pp.append(time.perf_counter() - a)
+    from celestia_da import blobfactory, square as gsq, testfactory
+    from celestia_da._lib import ptr
     W = 2 * k
+    ods = np.ascontiguousarray(np.stack([testfactory.random_square(k, 5000 + i) for i in range(n)]))
+    eds = np.ones((n, W * W * SHARE), dtype=np.uint8)
+    rows = np.ones((n, W * 90), dtype=np.uint8)
+    cols = np.ones((n, W * 90), dtype=np.uint8)
+    roots = np.ones((n, 32), dtype=np.uint8)
+    status = np.zeros(n, dtype=np.int32)
+    st = status.ctypes.data_as(C.POINTER(C.c_int32))
+
+    def run(with_eds, m=n):
+        ctx.check(ctx.lib.cda_extend_dah_batch(ctx.h, ptr(ods[:m]), k, m, ptr(eds[:m]) if with_eds else None,
+                                               ptr(rows[:m]), ptr(cols[:m]), ptr(roots[:m]), st))
+
+    def med(f):
+        f()
+        t = []
+        for _ in range(reps):
+            a = time.perf_counter()
+            f()
+            t.append(time.perf_counter() - a)
+        return sorted(t)[reps // 2]
+
+    full = med(lambda: run(True))
+    only_roots = med(lambda: run(False))
+    one = med(lambda: run(True, 1))
+    one_roots = med(lambda: run(False, 1))
+    txs = blobfactory.full_block(1, 128)
+    pp = med(lambda: gsq.construct_extend_dah(txs, 128, ctx=ctx))
     return {"k": k, "squares": n,
             "eds_to_host_squares_per_s": n / full,
-            "eds_to_host_gb_per_s": n * (k * k + W * W) * SHARE / full / 1e9,
-            "roots_only_squares_per_s": n / roots,
-            "process_proposal_ms": 1e3 * sorted(pp)[2],
-            "note": "cda_extend_dah_batch from pageable numpy buffers: H2D ODS + D2H EDS/roots inside the time; "
-                    "process_proposal_ms = cda_construct_extend_dah on a full k=128 block of blob txs "
-                    "(host txs -> data root, roots back to the host)"}
+            "pcie_gb_per_s": n * (k * k + 3 * k * k) * SHARE / full / 1e9,
+            "roots_only_squares_per_s": n / only_roots,
+            "one_square_eds_to_host_ms": 1e3 * one, "one_square_roots_only_ms": 1e3 * one_roots,
+            "process_proposal_ms": 1e3 * pp,
+            "note": "cda_extend_dah_batch with reused host buffers: H2D ODS, D2H of the three parity quadrants "
+                    "(the host copies Q0 from the ODS) overlapping the hashing, D2H roots; pcie_gb_per_s counts "
+                    "ODS in + parity out; process_proposal_ms = cda_construct_extend_dah on a full k=128 block of "
+                    "blob txs (host txs -> data root, roots back to the host)"}
 
 
 def cpu_model() -> str:

@@ -47,6 +47,8 @@ EXPORTED = (
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
     "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
+    "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_extend_dah_split", "cda_split_rows_send",
+    "cda_extend_dah_multi",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -147,6 +149,13 @@ def load():
         L.cda_nmt_prove_range.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                           C.c_uint32, u8p, u32p, u8p]
         L.cda_merkle_root.argtypes = [ctxp, u8p, u64p, C.c_uint32, u8p]
+        L.cda_comm_unique_id.argtypes = [u8p]
+        L.cda_comm_init.argtypes = [ctxp, C.c_int, C.c_int, u8p]
+        L.cda_comm_destroy.argtypes = [ctxp]
+        L.cda_extend_dah_split.argtypes = [ctxp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.cda_split_rows_send.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
+        L.cda_extend_dah_multi.argtypes = [C.POINTER(ctxp), C.c_uint32, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p,
+                                           u8p, i32p]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L
@@ -229,10 +238,59 @@ class Context:
         self.check(self.lib.cda_split_combine(self.h, d_row_sub, parts, k, d_col_slots, d_rows, d_cols, d_root,
                                               stream))
 
+    def split_rows_send(self, d_rows, k, n_rows, row0, parts, d_send, d_err, stream=None):
+        """Row block of n_rows ODS rows straight in the all-to-all send layout
+        [parts][R][C][512] (cda_split_rows_send)."""
+        self.check(self.lib.cda_split_rows_send(self.h, d_rows, k, n_rows, row0, parts, d_send, d_err, stream))
+
+    # -- multi-GPU inside the library (RCCL) --------------------------------
+    def comm_init(self, rank: int, world: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self.check(self.lib.cda_comm_init(self.h, rank, world, buf))
+
+    def comm_destroy(self):
+        self.check(self.lib.cda_comm_destroy(self.h))
+
+    def extend_dah_split(self, d_rows, k, d_col_block, d_row_roots, d_col_roots, d_root, d_err, stream=None):
+        """Config 5 on this rank with the library's own RCCL collectives."""
+        self.check(self.lib.cda_extend_dah_split(self.h, d_rows, k, d_col_block, d_row_roots, d_col_roots, d_root,
+                                                 d_err, stream))
+
     def push_order_detail(self):
         a, i, p = C.c_int32(), C.c_uint32(), C.c_uint32()
         self.lib.cda_push_order_detail(self.h, C.byref(a), C.byref(i), C.byref(p))
         return a.value, i.value, p.value
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (rank 0; hand the 128 bytes to every rank)."""
+    L = load()
+    buf = (C.c_uint8 * 128)()
+    rc = L.cda_comm_unique_id(buf)
+    if rc != CDA_OK:
+        raise CdaError(rc, L.cda_last_error(None).decode())
+    return bytes(buf)
+
+
+def extend_dah_multi(ctxs, ods: np.ndarray, want_eds: bool = True):
+    """Config 4 on one node: n squares (n, k*k, 512) split over the contexts
+    (one per GPU), run concurrently (cda_extend_dah_multi)."""
+    L = load()
+    ods = np.ascontiguousarray(ods, dtype=np.uint8)
+    n = ods.shape[0]
+    k = int(round((ods.size // (n * SHARE_SIZE)) ** 0.5))
+    W = 2 * k
+    eds = np.empty((n, W, W, SHARE_SIZE), dtype=np.uint8) if want_eds else None
+    rows = np.empty((n, W, NMT_ROOT_SIZE), dtype=np.uint8)
+    cols = np.empty((n, W, NMT_ROOT_SIZE), dtype=np.uint8)
+    roots = np.empty((n, 32), dtype=np.uint8)
+    status = np.empty(n, dtype=np.int32)
+    hs = (C.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+    rc = L.cda_extend_dah_multi(hs, len(ctxs), ptr(ods), k, n, ptr(eds), ptr(rows), ptr(cols), ptr(roots),
+                                status.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc not in (CDA_OK, CDA_ERR_PUSH_ORDER):
+        ctxs[0].check(rc)
+    return eds, rows, cols, roots, status
 
 
 _default = None

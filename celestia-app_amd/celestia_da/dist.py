@@ -7,10 +7,13 @@ Config 5 -- ONE square split across G ranks (one GPU each), row blocks then
 column blocks:
 
   1. rank g owns ODS rows [g*R, g*R+R), R = k/G: row-encode them (Q0 -> Q1)
-     and check their namespace order           -> row block R x W shares
+     and check their namespace order; the row block is written straight in
+     the all-to-all send layout [G][R][C] shares (cda_split_rows_send)
   2. all-to-all (RCCL over xGMI): rank g sends rank h the R x C slice of its
      row block for columns [h*C, h*C+C), C = W/G; every pair exchanges
-     R*C*512 bytes (4 MiB at k=512, G=8), one point-to-point link each
+     R*C*512 bytes (4 MiB at k=512, G=8), one point-to-point link each; the
+     received pieces are rows 0..k-1 of the column block as they land (no
+     host-side copies)
   3. rank h column-encodes its W x C block (Q0 -> Q2, Q1 -> Q3 -- equal to the
      reference's Q2 -> Q3 row extension by linearity), hashes every cell once,
      builds its C column roots and, for every EDS row, the NMT subtree node
@@ -22,7 +25,9 @@ column blocks:
 The EDS stays column-distributed (rank h holds full columns [h*C, h*C+C)).
 Compute is delegated to an `ops` object: `GpuSplitOps` (libcda.so) in
 production; the tests drive the same orchestration over gloo with a CPU
-implementation of the three steps to check the data movement.
+implementation of the three steps to check the data movement.  A host without
+torch.distributed runs the same split with the library's own RCCL
+communicator: `extend_dah_split_rccl` (cda_comm_init + cda_extend_dah_split).
 """
 from __future__ import annotations
 
@@ -51,6 +56,12 @@ class GpuSplitOps:
         block = t.empty((R, 2 * k, SHARE), dtype=t.uint8, device=self.device)
         self.ctx.split_rows(ods_rows.data_ptr(), k, R, row0, block.data_ptr(), err.data_ptr(), self._stream())
         return block
+
+    def rows_send(self, ods_rows, k, row0, parts, out, err):
+        """Row-encode into the send layout `out` = [parts][R][C][512]."""
+        R = ods_rows.numel() // (k * SHARE)
+        self.ctx.split_rows_send(ods_rows.data_ptr(), k, R, row0, parts, out.data_ptr(), err.data_ptr(),
+                                 self._stream())
 
     def cols(self, block, k, col0, err):
         t = self.torch
@@ -100,19 +111,16 @@ def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None, o
             return fallback()
 
     err = ops.new_err()
-    rb = local(lambda: ops.rows(ods_rows, k, rank * R, err),
-               lambda: torch.zeros((R, W, SHARE), dtype=torch.uint8, device=ods_rows.device))  # [R][W][512]
-    send = rb.view(R, world, C, SHARE).permute(1, 0, 2, 3).contiguous()        # [dst][R][C][512]
-    recv = torch.empty_like(send)                                               # [src][R][C][512]
+    dev = ods_rows.device
+    block = torch.empty((W, C, SHARE), dtype=torch.uint8, device=dev)       # my columns, all 2k rows
+    recv = block[:k].view(world, R, C, SHARE)                                # rank g's piece = rows g*R..g*R+R-1
+    send = torch.empty_like(recv) if world > 1 else recv                     # [dst][R][C][512]
+    local(lambda: ops.rows_send(ods_rows, k, rank * R, world, send, err), lambda: send.zero_())
     if world > 1:
         dist.all_to_all_single(recv, send, group=group)
-    else:
-        recv.copy_(send)
-    block = torch.empty((W, C, SHARE), dtype=torch.uint8, device=rb.device)
-    block[:k] = recv.reshape(k, C, SHARE)                                       # rows 0..k-1 of my columns
     col_slots, row_sub = local(lambda: ops.cols(block, k, rank * C, err),
-                               lambda: (torch.zeros((C, SLOT), dtype=torch.uint8, device=rb.device),
-                                        torch.zeros((W, SLOT), dtype=torch.uint8, device=rb.device)))
+                               lambda: (torch.zeros((C, SLOT), dtype=torch.uint8, device=dev),
+                                        torch.zeros((W, SLOT), dtype=torch.uint8, device=dev)))
     err = err.to(torch.int64) & 0xFFFFFFFF          # the kernels' uint32 word; MIN needs unsigned order
     if world > 1:
         dist.all_reduce(err, op=dist.ReduceOp.MIN, group=group)
@@ -129,7 +137,30 @@ def extend_dah_split(ods_rows, k: int, ops, rank: int, world: int, group=None, o
         col_all = torch.cat(cs).contiguous()                                    # [W][96]
         combined = local(lambda: ops.combine(row_sub_all, world, k, col_all), lambda: None)
         result = None if combined is None else (*combined, err)
-    return rb, block, result
+    return send, block, result
+
+
+def extend_dah_split_rccl(ctx, ods_rows, k: int, rank: int, world: int, stream=None):
+    """Config 5 through the library's own RCCL communicator (cda_comm_init must
+    have been called on `ctx` with this rank/world): returns (col_block,
+    result) with result = (row_roots, col_roots, data_root, err_word) on
+    rank 0, None elsewhere."""
+    import torch
+    dev = ods_rows.device
+    W = 2 * k
+    C = W // world
+    block = torch.empty((W, C, SHARE), dtype=torch.uint8, device=dev)
+    err = torch.empty((1,), dtype=torch.int32, device=dev)
+    rows = torch.empty((W, 90), dtype=torch.uint8, device=dev) if rank == 0 else None
+    cols = torch.empty((W, 90), dtype=torch.uint8, device=dev) if rank == 0 else None
+    root = torch.empty((32,), dtype=torch.uint8, device=dev) if rank == 0 else None
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    ctx.extend_dah_split(ods_rows.data_ptr(), k, block.data_ptr(), rows.data_ptr() if rank == 0 else None,
+                         cols.data_ptr() if rank == 0 else None, root.data_ptr() if rank == 0 else None,
+                         err.data_ptr(), stream)
+    result = (rows, cols, root, err.to(torch.int64) & 0xFFFFFFFF) if rank == 0 else None
+    return block, result
 
 
 def extend_dah_split_loopback(ods, k: int, parts: int, ops):

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <utility>
 
 #include "../../include/cda.h"
@@ -568,6 +569,95 @@ int cda_merkle_root(cda_ctx* ctx, const uint8_t* items, const uint64_t* off, uin
             if (off[i + 1] < off[i]) return e.fail(CDA_ERR_INVALID, "item offsets must be non-decreasing");
         return e.merkle_root(items, off, n, out);
     });
+}
+
+int cda_comm_unique_id(uint8_t* id) {
+    if (!id) return CDA_ERR_INVALID;
+    tl_err.msg.clear();
+    int rc = cda::comm_unique_id(id);
+    if (rc) tl_err.msg = "ncclGetUniqueId failed";
+    return rc;
+}
+
+int cda_comm_init(cda_ctx* ctx, int rank, int world, const uint8_t* id) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!id) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.comm_init(rank, world, id);
+    });
+}
+
+int cda_comm_destroy(cda_ctx* ctx) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        e.comm_destroy();
+        return CDA_OK;
+    });
+}
+
+int cda_split_rows_send(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
+                        uint32_t parts, void* d_send, uint32_t* d_err, void* stream) {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
+        if (!d_ods_rows || !d_send || !d_err) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.enqueue_split_rows_send(static_cast<const uint8_t*>(d_ods_rows), k, n_rows, row0, parts,
+                                         static_cast<uint8_t*>(d_send), d_err, s);
+    });
+}
+
+int cda_extend_dah_split(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, void* d_col_block, void* d_row_roots,
+                         void* d_col_roots, void* d_data_root, uint32_t* d_err, void* stream) {
+    return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
+        if (!d_ods_rows || !d_err) return e.fail(CDA_ERR_INVALID, "null buffer");
+        if (e.comm_rank() == 0 && (!d_row_roots || !d_col_roots || !d_data_root))
+            return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.split_extend_dah(static_cast<const uint8_t*>(d_ods_rows), k, static_cast<uint8_t*>(d_col_block),
+                                  static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
+                                  static_cast<uint8_t*>(d_data_root), d_err, s);
+    });
+}
+
+int cda_extend_dah_multi(cda_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* ods, uint32_t k, uint32_t n,
+                         uint8_t* eds, uint8_t* row_roots, uint8_t* col_roots, uint8_t* data_roots, int32_t* status) {
+    tl_err.msg.clear();
+    if (!ctxs || n_ctx == 0) {
+        tl_err.msg = "no contexts";
+        return CDA_ERR_INVALID;
+    }
+    if (n == 0) return CDA_OK;
+    const uint32_t W = 2 * k;
+    const size_t ods_sq = (size_t)k * k * CDA_SHARE_SIZE, eds_sq = (size_t)W * W * CDA_SHARE_SIZE;
+    const size_t roots_sq = (size_t)W * CDA_NMT_ROOT_SIZE;
+    std::vector<int> rcs(n_ctx, CDA_OK);
+    std::vector<std::string> msgs(n_ctx);
+    std::vector<std::thread> th;
+    uint32_t first = 0;
+    try {
+        for (uint32_t d = 0; d < n_ctx; d++) {
+            // context d: squares [first, first + m), config 4's contiguous shard
+            const uint32_t m = n / n_ctx + (d < n % n_ctx ? 1 : 0);
+            if (m == 0) continue;
+            th.emplace_back([=, &rcs, &msgs] {
+                rcs[d] = cda_extend_dah_batch(ctxs[d], ods + first * ods_sq, k, m,
+                                              eds ? eds + first * eds_sq : nullptr, row_roots + first * roots_sq,
+                                              col_roots + first * roots_sq, data_roots + (size_t)first * 32,
+                                              status ? status + first : nullptr);
+                msgs[d] = tl_err.msg;   // the worker thread's error text
+            });
+            first += m;
+        }
+    } catch (...) {
+        for (auto& t : th) t.join();
+        tl_err.msg = "thread creation failed";
+        return CDA_ERR_DEVICE;
+    }
+    for (auto& t : th) t.join();
+    // the first device error wins over push-order (reported per square in status)
+    int rc = CDA_OK;
+    for (uint32_t d = 0; d < n_ctx; d++) {
+        if (rcs[d] != CDA_OK && (rc == CDA_OK || rc == CDA_ERR_PUSH_ORDER) && rc != rcs[d]) {
+            rc = rcs[d];
+            tl_err.msg = msgs[d];
+        }
+    }
+    return rc;
 }
 
 int cda_set_profiling(cda_ctx* ctx, int enable) {

@@ -53,6 +53,9 @@ struct GatherPiece {
     uint32_t len;
 };
 
+// comm.hip: ncclGetUniqueId into 128 bytes (CDA_OK / CDA_ERR_DEVICE).
+int comm_unique_id(uint8_t* id);
+
 class Engine {
   public:
     explicit Engine(int device);
@@ -100,6 +103,17 @@ class Engine {
                            uint8_t* d_row_sub, uint32_t* d_err, hipStream_t s);
     int enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint32_t k, const uint8_t* d_col_slots,
                               uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_root, hipStream_t s);
+
+    // Config 5 inside the library (comm.hip): the row block written straight
+    // into the all-to-all send layout [parts][R][C][512], an RCCL
+    // communicator per context, and the whole split on the caller's stream.
+    int enqueue_split_rows_send(const uint8_t* d_rows, uint32_t k, uint32_t n_rows, uint32_t row0, uint32_t parts,
+                                uint8_t* d_send, uint32_t* d_err, hipStream_t s);
+    int comm_init(int rank, int world, const uint8_t* id);
+    void comm_destroy();
+    int comm_rank() const { return rank_; }
+    int split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_block, uint8_t* d_row_roots,
+                         uint8_t* d_col_roots, uint8_t* d_root, uint32_t* d_err, hipStream_t s);
 
     // Host-buffer helpers (copy in, run, copy out, synchronise).
     int host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
@@ -192,6 +206,12 @@ class Engine {
 
     int device_;
     hipStream_t stream_ = nullptr;
+    // host-buffer calls: device-to-host copies of the parity quadrants run on
+    // copy_out_ while stream_ hashes (ev_rs_: RS done, ev_out_: copies done)
+    hipStream_t copy_out_ = nullptr;
+    hipEvent_t ev_rs_ = nullptr, ev_out_ = nullptr;
+    int enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds);
+    static void copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds);
     hipEvent_t order_ev_ = nullptr;   // end of the last call's GPU work
     bool order_used_ = false;
     // Batch pipeline: RS of chunk i+1 (HBM/VALU mix) overlaps the SHA-256
@@ -226,6 +246,11 @@ class Engine {
     // standalone trees: host cells, all tree levels, axis indexes / error words, roots
     DevBuf tr_cells_, tr_levels_, tr_axis_, tr_roots_;
     DevBuf rs_pad_;   // Codec.Encode of a non-power-of-two shard count
+    // config 5 in the library: RCCL communicator (ncclComm_t), row block,
+    // send buffer, column block, slots
+    void* comm_ = nullptr;
+    int rank_ = 0, world_ = 0;
+    DevBuf split_blk_, split_send_, split_col_, split_slots_;
     int build_trees(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees, uint32_t square_size,
                     const uint32_t* axis, std::vector<uint64_t>* level_off, std::vector<uint32_t>* err_out);
     int tree_order_error(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,

@@ -54,7 +54,7 @@ Engine::~Engine() {
                       &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_, &cm_plan_, &cm_tables_,
                       &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_, &gf8_log_, &gf8_exp_, &gf8_skew_, &rp_cw_,
                       &rp_err_, &rp_present_, &rp_parity_, &rp_buf_, &rp_flags_, &tr_cells_, &tr_levels_,
-                      &tr_axis_, &tr_roots_, &rs_pad_})
+                      &tr_axis_, &tr_roots_, &rs_pad_, &split_blk_, &split_send_, &split_col_, &split_slots_})
         b->release();
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);
@@ -64,7 +64,11 @@ Engine::~Engine() {
     }
     for (hipEvent_t e : event_pool_) (void)hipEventDestroy(e);
     for (hipEvent_t e : sync_events_) (void)hipEventDestroy(e);
+    comm_destroy();
     if (order_ev_) (void)hipEventDestroy(order_ev_);
+    if (ev_rs_) (void)hipEventDestroy(ev_rs_);
+    if (ev_out_) (void)hipEventDestroy(ev_out_);
+    if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (rs_stream_) (void)hipStreamDestroy(rs_stream_);
     if (hash_stream_) (void)hipStreamDestroy(hash_stream_);
@@ -89,6 +93,9 @@ int Engine::init() {
     if ((rc = check(hipSetDevice(device_), "hipSetDevice"))) return rc;
     if ((rc = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
     if ((rc = check(hipEventCreateWithFlags(&order_ev_, hipEventDisableTiming), "hipEventCreate"))) return rc;
+    if ((rc = check(hipStreamCreateWithFlags(&copy_out_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if ((rc = check(hipEventCreateWithFlags(&ev_rs_, hipEventDisableTiming), "hipEventCreate"))) return rc;
+    if ((rc = check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority), so RS workgroups win free CU slots.
     // CDA_RS_CU=S:R[:G] (tuning): spatial split of the pipeline's streams.  CU
@@ -522,6 +529,37 @@ int Engine::push_order_error(const uint32_t* err_words, uint32_t n, const uint8_
     return CDA_OK;
 }
 
+// Host-buffer extension.  The EDS goes back over PCIe as its three parity
+// quadrants only: Q0 IS the caller's ODS, so the host copies it itself while
+// the GPU works (24 instead of 32 MiB over the link per k = 128 square), and
+// the parity copies start as soon as the RS launches finish, on copy_out_,
+// overlapping the NMT hashing on stream_.
+void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
+    const size_t row = (size_t)k * kShare, W = 2 * (size_t)k;
+    for (uint32_t sq = 0; sq < n; sq++)
+        for (uint32_t r = 0; r < k; r++)
+            memcpy(eds + ((size_t)sq * W * W + r * W) * kShare, ods + ((size_t)sq * k + r) * row, row);
+}
+
+int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds) {
+    const size_t W = 2 * (size_t)k, sq_b = W * W * kShare, half = k * W * kShare;
+    int rc;
+    if ((rc = check(hipEventRecord(ev_rs_, stream_), "hipEventRecord"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(copy_out_, ev_rs_, 0), "hipStreamWaitEvent"))) return rc;
+    for (uint32_t sq = 0; sq < n; sq++) {
+        // Q1: rows 0..k-1, columns k..2k-1 (strided); Q2|Q3: the bottom half
+        if ((rc = check(hipMemcpy2DAsync(eds + sq * sq_b + k * kShare, W * kShare, d_eds + sq * sq_b + k * kShare,
+                                         W * kShare, (size_t)k * kShare, k, hipMemcpyDeviceToHost, copy_out_),
+                        "D2H Q1")))
+            return rc;
+        if ((rc = check(hipMemcpyAsync(eds + sq * sq_b + half, d_eds + sq * sq_b + half, half, hipMemcpyDeviceToHost,
+                                       copy_out_),
+                        "D2H Q2|Q3")))
+            return rc;
+    }
+    return check(hipEventRecord(ev_out_, copy_out_), "hipEventRecord");
+}
+
 int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
                             uint8_t* roots, int32_t* status) {
     const uint32_t W = 2 * k;
@@ -536,17 +574,20 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     if ((rc = check(err_buf_.ensure((size_t)n * 4), "hipMalloc"))) return rc;
     hipStream_t s = stream_;
     if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
-    if ((rc = enqueue_extend_dah(h_ods_.as<uint8_t>(), k, n, h_eds_.as<uint8_t>(), h_rows_.as<uint8_t>(),
-                                 h_cols_.as<uint8_t>(), h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s)))
+    if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, n, h_eds_.as<uint8_t>(), s))) return rc;
+    if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, n, eds))) return rc;
+    if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, n, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
+                          h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s)))
         return rc;
-    if (eds && (rc = check(hipMemcpyAsync(eds, h_eds_.ptr, eds_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     if ((rc = check(hipMemcpyAsync(rows, h_rows_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     if ((rc = check(hipMemcpyAsync(cols, h_cols_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     if ((rc = check(hipMemcpyAsync(roots, h_roots_.ptr, (size_t)n * 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     std::vector<uint32_t> err(n);
     if ((rc = check(hipMemcpyAsync(err.data(), err_buf_.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H")))
         return rc;
+    if (eds) copy_q0(ods, k, n, eds);   // host work while the GPU runs
     if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    if (eds && (rc = check(hipEventSynchronize(ev_out_), "hipEventSynchronize"))) return rc;
     if (status)
         for (uint32_t i = 0; i < n; i++) status[i] = err[i] == 0xFFFFFFFFu ? CDA_OK : CDA_ERR_PUSH_ORDER;
     return push_order_error(err.data(), n, ods, k, false);
@@ -561,8 +602,9 @@ int Engine::host_extend(const uint8_t* ods, uint32_t k, uint8_t* eds) {
     hipStream_t s = stream_;
     if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
     if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, 1, h_eds_.as<uint8_t>(), s))) return rc;
-    if ((rc = check(hipMemcpyAsync(eds, h_eds_.ptr, eds_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
-    return check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if ((rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, 1, eds))) return rc;
+    copy_q0(ods, k, 1, eds);
+    return check(hipEventSynchronize(ev_out_), "hipEventSynchronize");
 }
 
 int Engine::host_dah(const uint8_t* eds, uint32_t k, uint8_t* rows, uint8_t* cols, uint8_t* root) {

@@ -41,6 +41,9 @@
  *                          Root / ProveRange (pkg/wrapper/nmt_wrapper.go:55-129)
  *   cda_merkle_root        go-square/merkle HashFromByteSlices (DAH.Hash for
  *                          any root count, data_availability_header.go:92-108)
+ *   cda_comm_* / cda_extend_dah_split / cda_extend_dah_multi
+ *                          multi-GPU configs 4 and 5 (app/process_proposal.go:138-152
+ *                          block replay; one square over G GPUs)
  *
  * Conventions
  *   - All buffers are plain byte arrays; shares are row-major and contiguous
@@ -183,6 +186,39 @@ int cda_split_cols(cda_ctx *ctx, void *d_col_block, uint32_t k, uint32_t n_cols,
 int cda_split_combine(cda_ctx *ctx, const void *d_row_subtree_slots, uint32_t parts, uint32_t k,
                       const void *d_col_root_slots, void *d_row_roots, void *d_col_roots, void *d_data_root,
                       void *stream);
+
+/* ---- Multi-GPU inside the library ---------------------------
+ * Config 5 with the library's own RCCL collectives (no torch.distributed in the
+ * host): rank 0 makes an id (cda_comm_unique_id, 128 bytes) and hands it to
+ * every rank out of band; each rank's context joins (cda_comm_init, one context
+ * per GPU, all ranks call it together); cda_extend_dah_split then runs the
+ * whole split of ONE square on `stream`: rows into the all-to-all send layout,
+ * a grouped ncclSend/ncclRecv all-to-all, column encode + hashing, a gather of
+ * the subtree / column-root slots and a MIN reduce of the push-order word to
+ * rank 0, which writes the roots and the data root.  Every rank must call it.
+ *   d_ods_rows: this rank's R = k/G ODS rows (R*k shares, device);
+ *   d_col_block: W x C shares (device, may be NULL = library scratch): the EDS
+ *     columns [rank*C, rank*C + C) on return (row-major [W][C][512]);
+ *   d_row_roots / d_col_roots (W*90) / d_data_root (32): rank 0 only;
+ *   d_err: one device uint32, on rank 0 the MIN over ranks of the push-order
+ *     words (0xFFFFFFFF = ordered; axis<<24 | index<<12 | position). */
+#define CDA_COMM_ID_BYTES 128
+int cda_comm_unique_id(uint8_t id[CDA_COMM_ID_BYTES]);
+int cda_comm_init(cda_ctx *ctx, int rank, int world, const uint8_t id[CDA_COMM_ID_BYTES]);
+int cda_comm_destroy(cda_ctx *ctx);
+int cda_extend_dah_split(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, void *d_col_block, void *d_row_roots,
+                         void *d_col_roots, void *d_data_root, uint32_t *d_err, void *stream);
+/* Step 1 of the split for a caller that runs its own all-to-all (e.g. over
+ * torch.distributed): the row block of R ODS rows written straight in the send
+ * layout [parts][R][C][512] (part h = columns [h*C, h*C + C)), so the received
+ * pieces ARE rows 0..k-1 of the receiver's column block. */
+int cda_split_rows_send(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
+                        uint32_t parts, void *d_send, uint32_t *d_err, void *stream);
+/* Config 4 on one node: n independent squares (host buffers, as
+ * cda_extend_dah_batch) split into contiguous shards over n_ctx contexts (one
+ * per GPU) and run concurrently on host threads; no collective. */
+int cda_extend_dah_multi(cda_ctx *const *ctxs, uint32_t n_ctx, const uint8_t *ods, uint32_t k, uint32_t n,
+                         uint8_t *eds, uint8_t *row_roots, uint8_t *col_roots, uint8_t *data_roots, int32_t *status);
 
 /* ---- Data-square construction ----------------------
  * go-square v1.1.0 square.Construct (mode CDA_SQUARE_CONSTRUCT; used by

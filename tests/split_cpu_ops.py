@@ -36,6 +36,11 @@ class CpuSplitOps:
                     self._lower(err, (0 << 24) | ((row0 + r) << 12) | (c + 1))
         return torch.from_numpy(out)
 
+    def rows_send(self, ods_rows, k, row0, parts, out, err):
+        rb = self.rows(ods_rows, k, row0, err)                      # [R][W][512]
+        R, W = rb.shape[0], rb.shape[1]
+        out.copy_(rb.view(R, parts, W // parts, SHARE).permute(1, 0, 2, 3))
+
     def cols(self, block, k, col0, err):
         b = block.numpy()
         W, C = b.shape[0], b.shape[1]

@@ -292,3 +292,82 @@ def test_codec_encode_non_power_of_two(ctx, k):
     rng = np.random.default_rng(k)
     data = rng.integers(0, 256, (k, 128), dtype=np.uint8)
     assert np.array_equal(rsmt2d.LeoRSCodec(ctx).encode(data), pyref.leopard_encode(data))
+
+
+def test_split_rows_send_layout_on_gpu(ctx):
+    """cda_split_rows_send writes the row block straight in the all-to-all
+    send layout [parts][R][C][512] (no host-side regrouping copies)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    k, parts, R = 32, 4, 8
+    W, C = 2 * k, 2 * k // 4
+    ods = coracle.random_square(k, 12).reshape(k, k, 512)
+    rows = torch.from_numpy(ods[8:16].copy()).to(dev)
+    err1 = torch.full((1,), -1, dtype=torch.int32, device=dev)
+    err2 = torch.full((1,), -1, dtype=torch.int32, device=dev)
+    blk = torch.empty((R, W, 512), dtype=torch.uint8, device=dev)
+    send = torch.empty((parts, R, C, 512), dtype=torch.uint8, device=dev)
+    ctx.split_rows(rows.data_ptr(), k, R, 8, blk.data_ptr(), err1.data_ptr())
+    ctx.split_rows_send(rows.data_ptr(), k, R, 8, parts, send.data_ptr(), err2.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(send, blk.view(R, parts, C, 512).permute(1, 0, 2, 3))
+    eds = coracle.extend(ods.reshape(-1, 512)).reshape(W, W, 512)
+    assert np.array_equal(blk.cpu().numpy(), eds[8:16])
+
+
+@pytest.mark.parametrize("k", [16, 512])
+def test_rccl_split_world1_on_gpu(ctx, k):
+    """Config 5 through the library's own RCCL communicator, world size 1
+    (RCCL self send/recv for the all-to-all and the gathers): EDS columns,
+    roots and data root equal the single-GPU path and the oracle."""
+    import torch
+    from celestia_da import _lib, dist as cdist, testfactory
+    dev = torch.device("cuda", 0)
+    c = _lib.Context(0)
+    c.comm_init(0, 1, _lib.comm_unique_id())
+    try:
+        ods = testfactory.random_square(k, 0 if k == 512 else 3)
+        d_ods = torch.from_numpy(ods).to(dev)
+        block, (rows, cols, root, err) = cdist.extend_dah_split_rccl(c, d_ods, k, 0, 1)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0xFFFFFFFF
+        W = 2 * k
+        e = torch.empty(W * W * 512, dtype=torch.uint8, device=dev)
+        r1 = torch.empty(W * 90, dtype=torch.uint8, device=dev)
+        c1 = torch.empty(W * 90, dtype=torch.uint8, device=dev)
+        g1 = torch.empty(32, dtype=torch.uint8, device=dev)
+        ctx.extend_dah_device(d_ods.data_ptr(), k, 1, e.data_ptr(), r1.data_ptr(), c1.data_ptr(), g1.data_ptr(),
+                              None, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(block.view(-1), e)
+        assert torch.equal(rows.view(-1), r1) and torch.equal(cols.view(-1), c1) and torch.equal(root, g1)
+        if k == 512:
+            import json, os
+            g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "k512.json")))
+            assert root.cpu().numpy().tobytes().hex() == g["squares"]["0"]["data_root"]
+        else:
+            assert root.cpu().numpy().tobytes() == coracle.extend_dah(ods)[3]
+    finally:
+        c.comm_destroy()
+        c.close()
+
+
+def test_extend_dah_multi_contexts(ctx):
+    """cda_extend_dah_multi (config 4 dispatcher): a host batch split over
+    two contexts (on the one GPU of the test box) equals the single-context
+    batch and the oracle."""
+    from celestia_da import _lib
+    k, n = 32, 5
+    ods = np.stack([coracle.random_square(k, 60 + i) for i in range(n)])
+    ctxs = [_lib.Context(0), _lib.Context(0)]
+    try:
+        eds, rows, cols, roots, status = _lib.extend_dah_multi(ctxs, ods)
+    finally:
+        for c in ctxs:
+            c.close()
+    e2, r2, c2, g2, s2 = da.extend_dah_batch(ods)
+    assert (status == 0).all()
+    assert np.array_equal(eds, e2) and np.array_equal(rows, r2) and np.array_equal(cols, c2)
+    assert np.array_equal(roots, g2)
+    for i in range(n):
+        assert roots[i].tobytes() == coracle.extend_dah(ods[i])[3]
