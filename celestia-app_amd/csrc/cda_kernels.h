@@ -105,6 +105,12 @@ struct Forest {
 };
 // One level of up to two forests with the same n_in (blockIdx.z selects).
 hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n_squares, hipStream_t stream);
+// Every remaining level of up to two forests of n_in (<= 256) nodes per tree
+// in one launch (a workgroup takes 256 / n_in trees, levels in LDS); the roots go to
+// roots / root_slots as in launch_level, and if dig is non-NULL their RFC-6962
+// leaf digests to dig[sq][root0 + t] (n_items per square).
+hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n_squares, uint32_t* dig,
+                           uint32_t n_items, hipStream_t stream);
 // RFC-6962 data root over n_items 96-B root slots per square (power of two).
 hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares, uint8_t* data_roots,
                             hipStream_t stream);

@@ -186,8 +186,12 @@ class Engine {
 
   private:
     int check(hipError_t e, const char* what);
+    // levels of the forests down to `stop` nodes per tree (f[i].in then
+    // describes that level); stop = 1 runs them all
     int run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
-                    uint64_t buf_sq, const uint64_t* out_off, hipStream_t s);
+                    uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop = 1);
+    uint32_t top_fuse_nodes(uint32_t W, uint32_t n) const;
+    int top_fuse_ = -1;   // CDA_TOP_FUSE (tuning / A-B): -1 auto, 0 off, N = nodes per tree
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,
                          bool src_is_eds);
 

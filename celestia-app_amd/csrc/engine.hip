@@ -138,6 +138,7 @@ int Engine::init() {
         (rc = check(hipStreamCreateWithFlags(&hash_stream_, hipStreamNonBlocking), "hipStreamCreate")))
         return rc;
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -198,6 +199,17 @@ Gf16Dev Engine::gf16(uint32_t k) const {
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+// Nodes per tree at which the NMT levels switch from one wide launch per level
+// to tree_top_kernel (0 = never): the first level whose parents, over all 2W
+// trees of the n squares, fill less than one wave per SIMD of the chip
+// (1024 SIMDs x 64 lanes).  CDA_TOP_FUSE=0 disables, =N forces N.
+uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n) const {
+    if (top_fuse_ >= 0) return (uint32_t)top_fuse_ <= W && top_fuse_ <= 256 ? (uint32_t)top_fuse_ : 0;
+    for (uint32_t m = W; m >= 2; m /= 2)
+        if ((uint64_t)n * 2 * W * (m / 2) < 65536) return m <= 256 ? m : 0;
+    return 0;
+}
 
 void Engine::order_begin(hipStream_t s) {
     if (order_used_) (void)hipStreamWaitEvent(s, order_ev_, 0);
@@ -270,10 +282,10 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
 // Run every level of `f` (n_forest forests of n_in leaves each) ping-ponging
 // between two scratch buffers; the first level reads f[i].in.
 int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
-                        uint64_t buf_sq, const uint64_t* out_off, hipStream_t s) {
+                        uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop) {
     uint8_t* out = bufA;
     int rc;
-    for (uint32_t m = n_in; m >= 2; m /= 2) {
+    for (uint32_t m = n_in; m >= 2 && m > stop; m /= 2) {
         for (uint32_t i = 0; i < n_forest; i++) {
             f[i].out = out + out_off[i];
             f[i].out_sq = buf_sq;
@@ -314,9 +326,23 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     f[1] = Forest{leaf_.as<uint8_t>(), slots_sq, W, 1, W, nullptr, 0, d_cols, (uint64_t)W * kNode,
                   root_slots_.as<uint8_t>(), (uint64_t)2 * W * kSlot, W};
     const uint64_t off[2] = {0, slots_sq / 2};
-    if ((rc = run_forests(f, 2, W, n, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), slots_sq, off, s))) return rc;
+    // Wide per-level launches while a level has at least a wave per SIMD of
+    // parents; the latency-bound rest of the trees (and the data root's RFC
+    // leaf digests) in one tree_top_kernel launch.
+    const uint32_t top = top_fuse_nodes(W, n);
+    if ((rc = run_forests(f, 2, W, n, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), slots_sq, off, s, top))) return rc;
+    if (top) {
+        if (d_roots && (rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
+        if ((rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig_.as<uint32_t>() : nullptr, 2 * W, s),
+                        "nmt tree top")))
+            return rc;
+    }
     mark_end(s);
-    if (d_roots) {   // NULL: roots only (repair verification needs no data root)
+    if (d_roots && top) {
+        mark_begin(kStageDataRoot, s);
+        if ((rc = check(launch_data_root_digests(dig_.as<uint32_t>(), 2 * W, n, d_roots, s), "data root"))) return rc;
+        mark_end(s);
+    } else if (d_roots) {   // NULL: roots only (repair verification needs no data root)
         mark_begin(kStageDataRoot, s);
         if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
         if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s),

@@ -18,6 +18,8 @@
 // once (4k^2 leaf hashes instead of the reference's 8k^2).  One thread per
 // leaf / per parent node; each NMT level of all 4k trees of every square in
 // the batch is one launch.  SHA-256 is pure 32-bit VALU work (no MFMA).
+#include <cstdlib>
+
 #include "cda_kernels.h"
 #include "sha256_dev.h"
 
@@ -206,6 +208,35 @@ struct Forest2 {
     Forest f[2];
 };
 
+// HashNode of two big-endian child slots -> parent slot (little-endian words,
+// as stored).  Block 0 = 0x01 || L[0:63]: a parity left child makes words
+// 0..13 constant, so those nodes start from the precomputed mid-state (MID).
+// The branch is worth it only where a wave's parents are all of one kind
+// (level_kernel orders them so); otherwise both paths run (MID = false).
+template <bool MID = true>
+__device__ __forceinline__ void hash_node(const uint32_t (&L)[kSlotWords], const uint32_t (&R)[kSlotWords],
+                                          uint32_t (&o)[kSlotWords]) {
+    uint32_t w[16];
+    ShaState st;
+    sha_init(st);
+    if (MID && is_parity_min(L)) {
+        w[14] = node_msg(L, R, 14);
+        w[15] = node_msg(L, R, 15);
+        sha_compress_from<kNodeParityRounds>(st, kNodeParityMid, kNodeParityHead, w);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, i);
+        sha_compress(st, w);
+    }
+#pragma unroll
+    for (int b = 1; b < 3; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
+        sha_compress(st, w);
+    }
+    inner_node_words(L, R, st.h, o);
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_WAVES))) void level_kernel(const Forest2 fs, uint32_t n_in) {
     const Forest& F = fs.f[blockIdx.z];
     const uint32_t n_out = n_in / 2;
@@ -231,29 +262,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
     const uint8_t* base = F.in + sq * F.in_sq;
     const uint8_t* l = base + ((size_t)t * F.tree_stride + (size_t)(2 * p) * F.node_stride) * kSlot;
     const uint8_t* rr = l + (size_t)F.node_stride * kSlot;
-    uint32_t L[kSlotWords], R[kSlotWords], w[16];
+    uint32_t L[kSlotWords], R[kSlotWords];
     load_slot_be(l, L);
     load_slot_be(rr, R);
-    ShaState st;
-    sha_init(st);
-    // block 0 = 0x01 || L[0:63]: a parity left child makes words 0..13 constant
-    if (is_parity_min(L)) {
-        w[14] = node_msg(L, R, 14);
-        w[15] = node_msg(L, R, 15);
-        sha_compress_from<kNodeParityRounds>(st, kNodeParityMid, kNodeParityHead, w);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, i);
-        sha_compress(st, w);
-    }
-#pragma unroll
-    for (int b = 1; b < 3; b++) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
-        sha_compress(st, w);
-    }
     uint32_t o[kSlotWords];
-    inner_node_words(L, R, st.h, o);
+    hash_node(L, R, o);
     if (n_out == 1) {
         if (F.roots) {
             uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
@@ -263,6 +276,85 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
         if (F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
     } else {
         store_slot(F.out + sq * F.out_sq + ((size_t)t * n_out + p) * kSlot, o);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused top of the trees (latency-bound part: fewer parents than the chip has
+// wave slots).  One workgroup per tree runs every remaining level in LDS, no
+// launch per level: the first level reads the tree's m input slots from
+// global memory, later levels ping-pong between two LDS halves.  The root goes
+// out packed (90 B) and as a 96-B slot like level_kernel's, and its RFC-6962
+// leaf digest sha256(0x00 || root) -- the first step of the data root -- is
+// computed in the same workgroup (dig[sq][root0 + t]), so the data root
+// continues with launch_data_root_digests.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kTopThreads = 128;   // one workgroup: tpw = 256 / n_in trees x n_in / 2 parents
+
+__global__ __launch_bounds__(kTopThreads) void tree_top_kernel(const Forest2 fs, uint32_t n_in, uint32_t tpw,
+                                                              uint32_t* __restrict__ dig, uint32_t n_items) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[2][kTopThreads][kSlotWords];
+    const size_t sq = blockIdx.y;
+    const uint32_t n_trees = fs.f[0].n_trees + fs.f[1].n_trees;
+    uint32_t o[kSlotWords];
+    uint32_t cur = 0;
+    for (uint32_t m = n_in; m >= 2; m /= 2) {
+        const uint32_t th = threadIdx.x, half = m / 2;
+        const uint32_t j = th / half, p = th % half;   // tree j of this workgroup, parent p
+        const uint32_t g = blockIdx.x * tpw + j;
+        if (j < tpw && g < n_trees) {
+            uint32_t L[kSlotWords], R[kSlotWords];
+            if (m == n_in) {
+                const bool f1 = g >= fs.f[0].n_trees;
+                const Forest& F = fs.f[f1 ? 1 : 0];
+                const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
+                const uint8_t* l =
+                    F.in + sq * F.in_sq + ((size_t)t * F.tree_stride + (size_t)(2 * p) * F.node_stride) * kSlot;
+                load_slot_be(l, L);
+                load_slot_be(l + (size_t)F.node_stride * kSlot, R);
+            } else {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) {
+                    L[i] = bswap32(buf[cur][j * m + 2 * p][i]);
+                    R[i] = bswap32(buf[cur][j * m + 2 * p + 1][i]);
+                }
+            }
+            hash_node<false>(L, R, o);   // a wave mixes data- and parity-left parents here
+            if (m > 2) {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][th][i] = o[i];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    // thread j < tpw holds tree j's root slot in o
+    const uint32_t g = blockIdx.x * tpw + threadIdx.x;
+    if (threadIdx.x >= tpw || g >= n_trees) return;
+    const bool f1 = g >= fs.f[0].n_trees;
+    const Forest& F = fs.f[f1 ? 1 : 0];
+    const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
+    if (F.roots) {
+        uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
+#pragma unroll
+        for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
+    }
+    if (F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
+    if (dig) {
+        uint32_t I[kSlotWords], w[16];
+#pragma unroll
+        for (int i = 0; i < kSlotWords; i++) I[i] = bswap32(o[i]);
+        ShaState st;
+        sha_init(st);
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+#pragma unroll
+            for (int jj = 0; jj < 16; jj++) w[jj] = rfc_leaf_msg(I, 16 * b + jj);
+            sha_compress(st, w);
+        }
+        uint4* d = reinterpret_cast<uint4*>(dig + (sq * n_items + F.root0 + t) * 8);
+        d[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+        d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
     }
 }
 
@@ -413,10 +505,25 @@ hipError_t launch_row_order(const CellGrid& g, uint32_t n, uint32_t* err, hipStr
     return hipGetLastError();
 }
 
+// Occupancy limiter (tuning / co-run experiments): CDA_HASH_LDS=N reserves N
+// bytes of (unused) LDS per hash workgroup, so at most 160 KiB / N of them
+// share a CU -- e.g. 98304 leaves room for exactly one 256-thread workgroup
+// (one wave per SIMD) next to a 64 KiB RS workgroup.
+static size_t hash_lds(const void* fn) {
+    static long v = -2;
+    if (v == -2) {
+        const char* e = getenv("CDA_HASH_LDS");
+        v = e ? atol(e) : 0;
+    }
+    if (v > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v);
+    return v > 0 ? (size_t)v : 0;
+}
+
 hipError_t launch_leaves(const CellGrid& g, uint32_t n, uint8_t* slots, uint32_t* err, bool check_rows,
                          bool check_cols, hipStream_t s) {
     dim3 grid((g.rows * g.cols + 255) / 256, n);
-    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), 0, s, g, slots, err, check_rows ? 1 : 0, check_cols ? 1 : 0);
+    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), hash_lds(reinterpret_cast<const void*>(leaf_kernel)), s, g,
+                       slots, err, check_rows ? 1 : 0, check_cols ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -429,7 +536,24 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
         maxw = maxw > f[i].n_trees * (n_in / 2) ? maxw : f[i].n_trees * (n_in / 2);
     }
     dim3 grid((maxw + 255) / 256, n, n_forest);
-    hipLaunchKernelGGL(level_kernel, grid, dim3(256), 0, s, fs, n_in);
+    hipLaunchKernelGGL(level_kernel, grid, dim3(256), hash_lds(reinterpret_cast<const void*>(level_kernel)), s, fs,
+                       n_in);
+    return hipGetLastError();
+}
+
+hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint32_t* dig,
+                           uint32_t n_items, hipStream_t s) {
+    if (n_forest < 1 || n_forest > 2 || n_in < 2 || n_in > 2 * kTopThreads || (n_in & (n_in - 1)))
+        return hipErrorInvalidValue;
+    Forest2 fs{};
+    uint32_t trees = 0;
+    for (uint32_t i = 0; i < n_forest; i++) {
+        fs.f[i] = f[i];
+        trees += f[i].n_trees;
+    }
+    const uint32_t tpw = 2 * kTopThreads / n_in;   // trees per workgroup
+    hipLaunchKernelGGL(tree_top_kernel, dim3((trees + tpw - 1) / tpw, n), dim3(kTopThreads), 0, s, fs, n_in, tpw, dig,
+                       n_items);
     return hipGetLastError();
 }
 
