@@ -289,40 +289,43 @@ def cpu_baseline(k: int, seconds: float, threads: int, runs: int = 5):
 
 def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
     """Config 5 timing: one k x k square split over `world`
-    GPUs.  Returns ms per square (max over ranks) and the data root; rank 0
-    also checks it against its single-GPU extend_dah of the same square."""
+    GPUs, by both drivers of the same kernels: the library's own RCCL
+    communicator (cda_comm_init + cda_extend_dah_split, what a cgo host uses)
+    and torch.distributed (celestia_da.dist.extend_dah_split).  Reports ms per
+    square (max over ranks); rank 0 checks both results against its
+    single-GPU extend_dah of the same square."""
     import torch
     import torch.distributed as dist
 
+    from celestia_da import _lib
     from celestia_da import dist as cdist
     from celestia_da import testfactory
 
     ods = testfactory.random_square(k, 0).reshape(k, k, SHARE)
     R = k // world
     mine = torch.from_numpy(ods[rank * R:(rank + 1) * R].copy()).to(dev)
-    ops = cdist.GpuSplitOps(ctx, dev)
-    errors = []
-    # every rank runs the same collectives even if a local step fails
-    res = cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append)          # warm-up
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        res = cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
     on = dev if dist.get_backend() == "nccl" else "cpu"
-    el = torch.tensor([time.perf_counter() - t0, float(len(errors))], dtype=torch.float64, device=on)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    if el[1].item() > 0:
-        return {"error": repr(errors[0]) if errors else "failed on another rank"}
-    out = {"k": k, "gpus": world, "ms_per_square": 1e3 * float(el[0].item()) / iters,
-           "squares_per_s": iters / float(el[0].item()),
-           "all_to_all_bytes_per_rank": (k // world) * (2 * k) * SHARE * (world - 1) // world}
+
+    def max_over_ranks(x: float, bad: int):
+        el = torch.tensor([x, float(bad)], dtype=torch.float64, device=on)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el[0].item()), el[1].item() > 0
+
+    def timed(run):
+        run()                                   # warm-up
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            res = run()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        return time.perf_counter() - t0, res
+
+    out = {"k": k, "gpus": world, "all_to_all_bytes_per_rank": R * (2 * k) * SHARE * (world - 1) // world}
+    W = 2 * k
+    ref = None
     if rank == 0:
-        rows, cols, root, err = res[2]
-        out["data_root"] = root.cpu().numpy().tobytes().hex()
-        W = 2 * k
         e = torch.empty(W * W * SHARE, dtype=torch.uint8, device=dev)
         r1 = torch.empty(W * 90, dtype=torch.uint8, device=dev)
         c1 = torch.empty(W * 90, dtype=torch.uint8, device=dev)
@@ -331,9 +334,44 @@ def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
         ctx.extend_dah_device(o.data_ptr(), k, 1, e.data_ptr(), r1.data_ptr(), c1.data_ptr(), g1.data_ptr(),
                               None, torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
-        out["matches_single_gpu"] = bool(torch.equal(g1, root) and torch.equal(r1.view(W, 90), rows)
-                                         and torch.equal(c1.view(W, 90), cols) and int(err.item()) == 0xFFFFFFFF)
-        del e
+        ref = (r1.view(W, 90), c1.view(W, 90), g1)
+        out["data_root"] = g1.cpu().numpy().tobytes().hex()
+        del e, o
+
+    def matches(res) -> bool:
+        rows, cols, root, err = res
+        return bool(torch.equal(ref[2], root) and torch.equal(ref[0], rows) and torch.equal(ref[1], cols)
+                    and int(err.item()) == 0xFFFFFFFF)
+
+    # (1) library RCCL communicator
+    try:
+        uid = torch.zeros(128, dtype=torch.uint8, device=on)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(_lib.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, src=0)
+        c = _lib.Context(dev.index)
+        c.comm_init(rank, world, bytes(uid.cpu().numpy()))
+        el, res = timed(lambda: cdist.extend_dah_split_rccl(c, mine, k, rank, world))
+        el, bad = max_over_ranks(el, 0)
+        out["library_rccl"] = {"ms_per_square": 1e3 * el / iters, "squares_per_s": iters / el}
+        if rank == 0:
+            out["library_rccl"]["matches_single_gpu"] = matches(res[1])
+        c.comm_destroy()
+        c.close()
+    except Exception as ex:  # report, keep the torch.distributed leg
+        out["library_rccl"] = {"error": f"{type(ex).__name__}: {ex}"}
+    # (2) torch.distributed collectives (every rank enters every collective even
+    # if a local step fails)
+    ops = cdist.GpuSplitOps(ctx, dev)
+    errors = []
+    el, res = timed(lambda: cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append))
+    el, bad = max_over_ranks(el, len(errors))
+    if bad:
+        out["torch_distributed"] = {"error": repr(errors[0]) if errors else "failed on another rank"}
+    else:
+        out["torch_distributed"] = {"ms_per_square": 1e3 * el / iters, "squares_per_s": iters / el}
+        if rank == 0:
+            out["torch_distributed"]["matches_single_gpu"] = matches(res[2])
     return out
 
 
@@ -573,6 +611,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all host CPUs (capped by OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip k=512 and latency extras")
+    ap.add_argument("--config5", action="store_true",
+                    help="run the config-5 extra (one k=512 square split over the ranks) even at one rank")
     ap.add_argument("--layout", choices=("packed", "inplace"), default="inplace",
                     help="inplace: ODS already in Q0 of the EDS arena (cda_extend_dah_inplace_device, the layout "
                          "rsmt2d's EDS has; no Q0 copy); packed: ODS in its own k*k buffer "
@@ -590,7 +630,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.config5:
+        if world == 1:   # a one-rank group for --config5 outside torchrun
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     k, B = args.k, args.batch
@@ -805,7 +850,7 @@ def main():
         extras["k512"]["batch2"] = {"squares_per_s": n5 * nb / elb, "ms_per_square": 1e3 * elb / (n5 * nb)}
         del eb
 
-    if world > 1 and not args.no_extras:
+    if (world > 1 or args.config5) and not args.no_extras:
         # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
         # all-to-all of the row-encoded blocks, column encode + hashing per
         # rank, gather of subtree/column roots, combine on rank 0).
@@ -847,7 +892,7 @@ def main():
             "extras": extras,
         }
         print(json.dumps(line))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

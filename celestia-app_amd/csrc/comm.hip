@@ -104,7 +104,7 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
     const size_t piece = (size_t)R * C * kShare;   // one rank pair's all-to-all block
     ncclComm_t comm = static_cast<ncclComm_t>(comm_);
     int rc;
-    if ((rc = check(split_send_.ensure(piece * G), "hipMalloc send"))) return rc;
+    if (G > 1 && (rc = check(split_send_.ensure(piece * G), "hipMalloc send"))) return rc;
     uint8_t* block = d_col_block;
     if (!block) {
         if ((rc = check(split_col_.ensure((size_t)W * C * kShare), "hipMalloc column block"))) return rc;
@@ -119,19 +119,27 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
     uint8_t* g_sub = col_slots + own;                        // [G][W][96]
     uint8_t* g_col = g_sub + (size_t)G * W * kSlot;          // [G*C = W][96]
     if ((rc = check(hipMemsetAsync(d_err, 0xFF, 4, s), "hipMemsetAsync"))) return rc;
-    // 1. rows -> [G][R][C] send layout
-    if ((rc = enqueue_split_rows_send(d_rows, k, R, (uint32_t)rank_ * R, G, split_send_.as<uint8_t>(), d_err, s)))
-        return rc;
-    // 2. all-to-all: piece h goes to rank h, rank g's piece lands at rows g*R..g*R+R-1 of the column block
-    if ((rc = nccl_check(*this, ncclGroupStart(), "ncclGroupStart"))) return rc;
-    for (uint32_t h = 0; h < G; h++) {
-        if ((rc = nccl_check(*this, ncclSend(split_send_.as<uint8_t>() + h * piece, piece, ncclUint8, (int)h, comm, s),
-                             "ncclSend")))
+    if (G == 1) {
+        // one rank: the row block IS rows 0..k-1 of the (whole) column block
+        if ((rc = enqueue_split_rows_send(d_rows, k, R, 0, 1, block, d_err, s))) return rc;
+    } else {
+        // 1. rows -> [G][R][C] send layout
+        if ((rc = enqueue_split_rows_send(d_rows, k, R, (uint32_t)rank_ * R, G, split_send_.as<uint8_t>(), d_err,
+                                          s)))
             return rc;
-        if ((rc = nccl_check(*this, ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s), "ncclRecv")))
-            return rc;
+        // 2. all-to-all: piece h goes to rank h; rank g's piece lands at rows
+        //    g*R..g*R+R-1 of the column block
+        if ((rc = nccl_check(*this, ncclGroupStart(), "ncclGroupStart"))) return rc;
+        for (uint32_t h = 0; h < G; h++) {
+            if ((rc = nccl_check(*this,
+                                 ncclSend(split_send_.as<uint8_t>() + h * piece, piece, ncclUint8, (int)h, comm, s),
+                                 "ncclSend")))
+                return rc;
+            if ((rc = nccl_check(*this, ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s), "ncclRecv")))
+                return rc;
+        }
+        if ((rc = nccl_check(*this, ncclGroupEnd(), "ncclGroupEnd"))) return rc;
     }
-    if ((rc = nccl_check(*this, ncclGroupEnd(), "ncclGroupEnd"))) return rc;
     // 3. columns: Q2|Q3 parity, leaves, column roots, row subtrees
     if ((rc = enqueue_split_cols(block, k, C, (uint32_t)rank_ * C, col_slots, row_sub, d_err, s))) return rc;
     // 4. gather the slots on rank 0 and reduce the push-order word

@@ -371,3 +371,22 @@ def test_extend_dah_multi_contexts(ctx):
     assert np.array_equal(roots, g2)
     for i in range(n):
         assert roots[i].tobytes() == coracle.extend_dah(ods[i])[3]
+
+
+@pytest.mark.parametrize("k", [8, 128])
+def test_torch_split_world1_rows_send_on_gpu(ctx, k):
+    """celestia_da.dist.extend_dah_split at one rank with the GPU ops: the row
+    encode writes straight into the column block (cda_split_rows_send), no
+    collective runs; result equals the oracle."""
+    import torch
+    from celestia_da import dist as cdist
+    dev = torch.device("cuda", 0)
+    ods = coracle.random_square(k, 21)
+    send, block, (rows, cols, root, err) = cdist.extend_dah_split(torch.from_numpy(ods).to(dev), k,
+                                                                   cdist.GpuSplitOps(ctx, dev), 0, 1)
+    torch.cuda.synchronize()
+    e_eds, e_rows, e_cols, e_root = coracle.extend_dah(ods) if k < 64 else coracle.cpu_baseline(ods, 8)
+    assert int(err.item()) == 0xFFFFFFFF
+    assert np.array_equal(block.cpu().numpy().reshape(-1, 512), e_eds)
+    assert np.array_equal(rows.cpu().numpy(), e_rows) and np.array_equal(cols.cpu().numpy(), e_cols)
+    assert root.cpu().numpy().tobytes() == e_root
