@@ -118,12 +118,16 @@ hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_
 // (one thread per root, into `digests`: n_items*n_squares*32 B of scratch),
 // then one workgroup per square for the inner levels (n_items a power of two
 // <= 4096).
+// err / status (optional): also writes status[sq] = CDA_OK / CDA_ERR_PUSH_ORDER
+// from the push-order word err[sq] (status_kernel fused into the last launch).
 hipError_t launch_data_root_slots(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares,
-                                  uint32_t* digests, uint8_t* data_roots, hipStream_t stream);
+                                  uint32_t* digests, uint8_t* data_roots, hipStream_t stream,
+                                  const uint32_t* err = nullptr, int32_t* status = nullptr);
 // RFC-6962 leaf digests sha256(0x00 || slot[0:90]) of n slots (8 words each).
 hipError_t launch_rfc_leaves(const uint8_t* slots, uint32_t n, uint32_t* digests, hipStream_t stream);
 hipError_t launch_data_root_digests(const uint32_t* digests, uint32_t n_items, uint32_t n_squares,
-                                    uint8_t* data_roots, hipStream_t stream);
+                                    uint8_t* data_roots, hipStream_t stream, const uint32_t* err = nullptr,
+                                    int32_t* status = nullptr);
 // Pack n_slots 96-B root slots (rows then columns) into 90-B roots.
 hipError_t launch_slots_to_roots(const uint8_t* slots, uint32_t n_slots, uint8_t* rows, uint8_t* cols, uint32_t w,
                                  hipStream_t stream);

@@ -338,19 +338,23 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
             return rc;
     }
     mark_end(s);
+    // the data-root launch also writes the per-square push-order status
     if (d_roots && top) {
         mark_begin(kStageDataRoot, s);
-        if ((rc = check(launch_data_root_digests(dig_.as<uint32_t>(), 2 * W, n, d_roots, s), "data root"))) return rc;
+        if ((rc = check(launch_data_root_digests(dig_.as<uint32_t>(), 2 * W, n, d_roots, s, d_err, d_status),
+                        "data root")))
+            return rc;
         mark_end(s);
     } else if (d_roots) {   // NULL: roots only (repair verification needs no data root)
         mark_begin(kStageDataRoot, s);
         if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
-        if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s),
+        if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s,
+                                               d_err, d_status),
                         "data root")))
             return rc;
         mark_end(s);
     }
-    if (d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
+    if (!d_roots && d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
     return CDA_OK;
 }
 

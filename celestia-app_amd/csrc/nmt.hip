@@ -219,6 +219,10 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kSlotWords], const
     uint32_t w[16];
     ShaState st;
     sha_init(st);
+    // (Writing the parity branch's constant 0xFF words of blocks 1-2 as
+    // literals saves ~1.5% of its rotations but duplicates blocks 1-2 per
+    // branch: ~8.2k instead of ~5.5k instructions, past the instruction cache
+    // a CU pair shares -- not taken.)
     if (MID && is_parity_min(L)) {
         w[14] = node_msg(L, R, 14);
         w[15] = node_msg(L, R, 15);
@@ -434,7 +438,9 @@ __global__ __launch_bounds__(256) void rfc_leaf_kernel(const uint8_t* __restrict
 // workgroup per square, n/2 threads (<= 1024) hash the first inner level
 // straight from global memory, later levels ping-pong in LDS.
 __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
-                                                               uint8_t* __restrict__ data_roots) {
+                                                               uint8_t* __restrict__ data_roots,
+                                                               const uint32_t* __restrict__ err,
+                                                               int32_t* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [n/2][8] | [n/4][8]
     const size_t sq = blockIdx.x;
     const uint32_t* D = dig + sq * (size_t)n * 8;
@@ -467,6 +473,8 @@ __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* 
         uint32_t* o = reinterpret_cast<uint32_t*>(data_roots + sq * 32);
 #pragma unroll
         for (int j = 0; j < 8; j++) o[j] = bswap32(src[j]);
+        // the push-order status of the square (status_kernel, fused: one launch less)
+        if (status) status[sq] = err[sq] == 0xFFFFFFFFu ? 0 : -3;   // CDA_OK / CDA_ERR_PUSH_ORDER
     }
 }
 
@@ -572,13 +580,13 @@ hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_
 }
 
 hipError_t launch_data_root_slots(const uint8_t* root_slots, uint32_t n_items, uint32_t n, uint32_t* dig,
-                                  uint8_t* data_roots, hipStream_t s) {
+                                  uint8_t* data_roots, hipStream_t s, const uint32_t* err, int32_t* status) {
     if (n_items < 2 || n_items > 4096 || (n_items & (n_items - 1))) return hipErrorInvalidValue;
     const uint32_t total = n_items * n;
     hipLaunchKernelGGL(rfc_leaf_kernel, dim3((total + 255) / 256), dim3(256), 0, s, root_slots, total, dig);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_data_root_digests(dig, n_items, n, data_roots, s);
+    return launch_data_root_digests(dig, n_items, n, data_roots, s, err, status);
 }
 
 hipError_t launch_rfc_leaves(const uint8_t* slots, uint32_t n, uint32_t* dig, hipStream_t s) {
@@ -588,7 +596,7 @@ hipError_t launch_rfc_leaves(const uint8_t* slots, uint32_t n, uint32_t* dig, hi
 }
 
 hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint32_t n, uint8_t* data_roots,
-                                    hipStream_t s) {
+                                    hipStream_t s, const uint32_t* err, int32_t* status) {
     if (n_items < 2 || n_items > 4096 || (n_items & (n_items - 1))) return hipErrorInvalidValue;
     const size_t lds = (size_t)(n_items / 2 + n_items / 4) * 32;
     if (lds > 64 * 1024) {
@@ -597,7 +605,8 @@ hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint3
         if (e != hipSuccess) return e;
     }
     const uint32_t threads = n_items / 2 < 1024 ? (n_items / 2 < 64 ? 64 : n_items / 2) : 1024;
-    hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots);
+    hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots,
+                       status ? err : nullptr, status);
     return hipGetLastError();
 }
 
