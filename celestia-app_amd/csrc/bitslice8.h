@@ -214,6 +214,80 @@ BS_HD void pass_b(uint32_t* R) {
     });
 }
 
+// ---- half layout (rs8_bs_half_kernel): a lane holds 8 of the 16 shards of
+// block U, the ones of its parity h (shard 16U + 2j + h in R[8j + p],
+// j = 0..7), and its partner lane the other 8.  The IFFT / FFT layers of shard
+// distance 2, 4, 8 pair registers of one lane (distance 1, 2, 4) and use the
+// same constant in both lanes, so they stay wave-uniform and compile-time;
+// only shard distance 1 pairs the two lanes (the *_d1 steps below, given the
+// partner's planes P).
+template <int U>
+BS_HD void pass_a_hi(uint32_t* R) {   // IFFT shard distance 2, 4, 8
+    sfor<0, 3, 1>([&](auto ld) {
+        constexpr int dj = 1 << decltype(ld)::value;
+        sfor<0, 8, 2 * dj>([&](auto gg) {
+            constexpr int gj = decltype(gg)::value;
+            constexpr uint32_t L = kField.skew[K - 1 + 16 * U + 2 * gj + 2 * dj];
+            sfor<gj, gj + dj, 1>([&](auto ii) {
+                constexpr int i = decltype(ii)::value;
+                ifft_bfly<L>(R + 8 * i, R + 8 * (i + dj));
+            });
+        });
+    });
+}
+template <int U>
+BS_HD void pass_c_hi(uint32_t* R) {   // FFT shard distance 8, 4, 2
+    sfor<0, 3, 1>([&](auto ld) {
+        constexpr int dj = 4 >> decltype(ld)::value;
+        sfor<0, 8, 2 * dj>([&](auto gg) {
+            constexpr int gj = decltype(gg)::value;
+            constexpr uint32_t L = kField.skew[16 * U + 2 * gj + 2 * dj - 1];
+            sfor<gj, gj + dj, 1>([&](auto ii) {
+                constexpr int i = decltype(ii)::value;
+                fft_bfly<L>(R + 8 * i, R + 8 * (i + dj));
+            });
+        });
+    });
+}
+// x ^ (p & m)
+BS_HD uint32_t xor_and(uint32_t x, uint32_t p, uint32_t m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(x, p, m, 0x78);
+#else
+    return x ^ (p & m);
+#endif
+}
+// IFFT butterfly of shards (2j, 2j+1) across the lane pair: x = own planes,
+// P = the partner's, h0 = all-ones in the lane holding the even shard.  Both
+// lanes form y' = x ^ y; the even lane keeps x ^ c*y', the odd lane y'.
+template <uint32_t L>
+BS_HD void ifft_d1(uint32_t* x, const uint32_t* P, uint32_t h0) {
+    uint32_t T[8];
+#pragma unroll
+    for (int p = 0; p < 8; p++) T[p] = x[p] ^ P[p];
+    if constexpr (L != kMod) mul_add<L>(x, T);
+#pragma unroll
+    for (int p = 0; p < 8; p++) x[p] = bitsel(x[p], T[p], h0);
+    fence<8>(x);
+}
+// FFT butterfly across the lane pair: even lane x' = x ^ c*y (y = P), odd
+// lane y' = y ^ x' = y ^ x ^ c*y (y = own): acc = own ^ (P & h1), acc ^= c*Y.
+template <uint32_t L>
+BS_HD void fft_d1(uint32_t* x, const uint32_t* P, uint32_t h0) {
+    uint32_t Y[8];
+#pragma unroll
+    for (int p = 0; p < 8; p++) {
+        Y[p] = bitsel(P[p], x[p], h0);
+        x[p] = xor_and(x[p], P[p], ~h0);
+    }
+    if constexpr (L != kMod) mul_add<L>(x, Y);
+    fence<8>(x);
+}
+template <int U>
+constexpr uint32_t ifft_d1_log(int j) { return kField.skew[K - 1 + 16 * U + 2 * j + 1]; }
+template <int U>
+constexpr uint32_t fft_d1_log(int j) { return kField.skew[16 * U + 2 * j]; }
+
 // Runs f(integral_constant<U>) for U == u as a chain of uniform if-blocks.
 template <class F>
 BS_HD void with_u_chain(uint32_t u, F&& f) {

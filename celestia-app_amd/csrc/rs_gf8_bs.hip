@@ -40,7 +40,17 @@ using namespace bs8;
 
 constexpr uint32_t kLdsBytes = 8 * 8 * 8 * 64 * 4;   // E[u][tt][p][lane] dwords
 
+// Timing-diagnostic builds only (tools/rs8_phase_probe.sh, wrong output):
+// CDA_RS8_PROBE=1 drops the XOR networks and transposes (memory + exchange
+// phases alone), =2 drops the global loads and stores (compute + exchange),
+// =3 drops the LDS exchanges, =4 makes the kernel a no-op (hash stages alone).
+#ifndef CDA_RS8_PROBE
+#define CDA_RS8_PROBE 0
+#endif
+constexpr bool kCompute = CDA_RS8_PROBE != 1, kMemory = CDA_RS8_PROBE != 2, kExchange = CDA_RS8_PROBE != 3;
+
 __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob job) {
+    if constexpr (CDA_RS8_PROBE == 4) return;
     extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = threadIdx.x & 63;
@@ -66,13 +76,18 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
     // ---- pass A --------------------------------------------------------
 #pragma unroll
     for (int t = 0; t < 16; t++) {
+        if constexpr (!kMemory) {
+#pragma unroll
+            for (int p = 0; p < 8; p++) R[8 * t + p] = (threadIdx.x + 977u * blockIdx.x) * (8u * t + p + 1u);
+            continue;
+        }
         const uint32_t o = s0 + (16 * u + t) * g.src_sh;
         const uint4 a = *reinterpret_cast<const uint4*>(src + o);
         const uint4 b = *reinterpret_cast<const uint4*>(src + o + 256);
         R[8 * t + 0] = a.x; R[8 * t + 1] = a.y; R[8 * t + 2] = a.z; R[8 * t + 3] = a.w;
         R[8 * t + 4] = b.x; R[8 * t + 5] = b.y; R[8 * t + 6] = b.z; R[8 * t + 7] = b.w;
     }
-    if (g.cpy_off != kNoCopy) {
+    if (kMemory && g.cpy_off != kNoCopy) {
         const uint32_t c0 = g.cpy_off + c * g.cpy_cw + col;
 #pragma unroll
         for (int t = 0; t < 16; t++) {
@@ -82,13 +97,15 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
                 make_uint4(R[8 * t + 4], R[8 * t + 5], R[8 * t + 6], R[8 * t + 7]);
         }
     }
+    if constexpr (kCompute) {
 #pragma unroll
-    for (int t = 0; t < 16; t++) transpose8(R + 8 * t);
-    with_u_chain(ud, [&](auto U) { pass_a<decltype(U)::value>(R); });
+        for (int t = 0; t < 16; t++) transpose8(R + 8 * t);
+        with_u_chain(ud, [&](auto U) { pass_a<decltype(U)::value>(R); });
+    }
 
     // ---- A -> B: round r moves t = 8r + tt (tt = 0..7) ---------------------
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
+    for (int r = 0; r < (kExchange ? 2 : 0); r++) {
         if (r) __syncthreads();
 #pragma unroll
         for (int tt = 0; tt < 8; tt++)
@@ -101,11 +118,13 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
             for (int p = 0; p < 8; p++) R[64 * r + 8 * uu + p] = E[((uu * 8 + w) * 8 + p) * 64 + l];
     }
     // ---- pass B: units t = w (R[0..64)) and t = w + 8 (R[64..128)) ---------
-    pass_b(R);
-    pass_b(R + 64);
+    if constexpr (kCompute) {
+        pass_b(R);
+        pass_b(R + 64);
+    }
     // ---- B -> C ------------------------------------------------------------
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
+    for (int r = 0; r < (kExchange ? 2 : 0); r++) {
         __syncthreads();
 #pragma unroll
         for (int uu = 0; uu < 8; uu++)
@@ -118,21 +137,165 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
             for (int p = 0; p < 8; p++) R[8 * (8 * r + tt) + p] = E[((u * 8 + tt) * 8 + p) * 64 + l];
     }
     // ---- pass C --------------------------------------------------------
-    with_u_chain(ud, [&](auto U) { pass_c<decltype(U)::value>(R); });
+    if constexpr (kCompute) with_u_chain(ud, [&](auto U) { pass_c<decltype(U)::value>(R); });
+    if constexpr (!kMemory) {   // keep every result live: a store no input can trigger
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 128; i++) acc ^= R[i] * (uint32_t)(2 * i + 1);
+        if (acc == 0x9E3779B9u && threadIdx.x == 511u) dst[d0] = (uint8_t)acc;
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < 16; t++) {
-        transpose8(R + 8 * t);
+        if constexpr (kCompute) transpose8(R + 8 * t);
         const uint32_t o = d0 + (16 * u + t) * g.dst_sh;
         *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * t], R[8 * t + 1], R[8 * t + 2], R[8 * t + 3]);
         *reinterpret_cast<uint4*>(dst + o + 256) = make_uint4(R[8 * t + 4], R[8 * t + 5], R[8 * t + 6], R[8 * t + 7]);
     }
 }
 
+// ---------------------------------------------------------------------------
+// Half-footprint variant: one 512-thread workgroup encodes 2 codewords x 512
+// columns.  Lane l of wave u owns codeword l/32, shard parity h = (l/16)&1 and
+// the same 32 columns as above (16*(l%16) ..), i.e. shards 16u + 2j + h,
+// j = 0..7: 64 data VGPRs instead of 128, so a CU holds two workgroups at four
+// waves per SIMD and one workgroup's loads and stores overlap the other's XOR
+// networks (rs8_bs_kernel alternates load -> compute -> store per CU:
+// profiles/r02_rs8_phases.txt).  Shard distance 1 pairs lane l with l ^ 16
+// (ds_swizzle); every other layer stays in-lane (bitslice8.h pass_*_hi).  The
+// exchanges move half the planes per round through 64 KiB of LDS.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHalfLdsBytes = 8 * 8 * 4 * 64 * 4;   // E[a][b][4 planes][lane] dwords
+
+__device__ __forceinline__ uint32_t swap16(uint32_t v) {   // lane l <- lane l ^ 16
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // bit mode: and 0x1F, xor 0x10
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job) {
+    extern __shared__ uint32_t E[];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t l = threadIdx.x & 63;
+    const uint32_t h = (l >> 4) & 1;
+    const uint32_t h0 = h ? 0u : 0xFFFFFFFFu;
+    const uint32_t cwg = 2 * blockIdx.x;
+    const bool s1 = job.n_seg > 1 && cwg >= job.seg[0].n_cw;
+    const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
+    const uint32_t c = (s1 ? cwg - job.seg[0].n_cw : cwg) + (l >> 5);
+    const uint32_t col = 16 * (l & 15);
+    const uint8_t* src = job.src + blockIdx.y * job.src_sq;
+    uint8_t* dst = job.dst + blockIdx.y * job.dst_sq;
+    const uint32_t u = w;
+    const uint32_t s0 = g.src_off + c * g.src_cw + col + (16 * u + h) * g.src_sh;   // shard 16u + h
+    const uint32_t d0 = g.dst_off + c * g.dst_cw + col + (16 * u + h) * g.dst_sh;
+    uint32_t ud = threadIdx.x >> 6;   // divergent copy of u for the per-U chains (see rs8_bs_kernel)
+    asm volatile("" : "+v"(ud));
+
+    uint32_t R[64];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t o = s0 + 2 * j * g.src_sh;
+        const uint4 a = *reinterpret_cast<const uint4*>(src + o);
+        const uint4 b = *reinterpret_cast<const uint4*>(src + o + 256);
+        R[8 * j + 0] = a.x; R[8 * j + 1] = a.y; R[8 * j + 2] = a.z; R[8 * j + 3] = a.w;
+        R[8 * j + 4] = b.x; R[8 * j + 5] = b.y; R[8 * j + 6] = b.z; R[8 * j + 7] = b.w;
+    }
+    if (g.cpy_off != kNoCopy) {
+        const uint32_t c0 = g.cpy_off + c * g.cpy_cw + col + (16 * u + h) * g.cpy_sh;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t o = c0 + 2 * j * g.cpy_sh;
+            *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * j], R[8 * j + 1], R[8 * j + 2], R[8 * j + 3]);
+            *reinterpret_cast<uint4*>(dst + o + 256) =
+                make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) transpose8(R + 8 * j);
+    // ---- pass A: IFFT shard distance 1 (across the lane pair), then 2, 4, 8
+    with_u_chain(ud, [&](auto U) {
+        constexpr int UU = decltype(U)::value;
+        sfor<0, 8, 1>([&](auto jj) {
+            constexpr int j = decltype(jj)::value;
+            uint32_t P[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) P[p] = swap16(R[8 * j + p]);
+            ifft_d1<ifft_d1_log<UU>(j)>(R + 8 * j, P, h0);
+        });
+        pass_a_hi<UU>(R);
+    });
+    // ---- A -> B: register j of wave u -> register u of wave j; round r moves
+    // planes 4r..4r+3 (slot [a][b] = pass-A wave b's register a)
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        if (r) __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+#pragma unroll
+            for (int pp = 0; pp < 4; pp++) E[((j * 8 + u) * 4 + pp) * 64 + l] = R[8 * j + 4 * r + pp];
+        __syncthreads();
+#pragma unroll
+        for (int uu = 0; uu < 8; uu++)
+#pragma unroll
+            for (int pp = 0; pp < 4; pp++) R[8 * uu + 4 * r + pp] = E[((w * 8 + uu) * 4 + pp) * 64 + l];
+    }
+    // ---- pass B: shards 16u + 2w + h of every u (R[8u + p])
+    pass_b(R);
+    // ---- B -> A
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        __syncthreads();
+#pragma unroll
+        for (int uu = 0; uu < 8; uu++)
+#pragma unroll
+            for (int pp = 0; pp < 4; pp++) E[((w * 8 + uu) * 4 + pp) * 64 + l] = R[8 * uu + 4 * r + pp];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+#pragma unroll
+            for (int pp = 0; pp < 4; pp++) R[8 * j + 4 * r + pp] = E[((j * 8 + u) * 4 + pp) * 64 + l];
+    }
+    // ---- pass C: FFT shard distance 8, 4, 2, then 1 across the lane pair
+    with_u_chain(ud, [&](auto U) {
+        constexpr int UU = decltype(U)::value;
+        pass_c_hi<UU>(R);
+        sfor<0, 8, 1>([&](auto jj) {
+            constexpr int j = decltype(jj)::value;
+            uint32_t P[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) P[p] = swap16(R[8 * j + p]);
+            fft_d1<fft_d1_log<UU>(j)>(R + 8 * j, P, h0);
+        });
+    });
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        transpose8(R + 8 * j);
+        const uint32_t o = d0 + 2 * j * g.dst_sh;
+        *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * j], R[8 * j + 1], R[8 * j + 2], R[8 * j + 3]);
+        *reinterpret_cast<uint4*>(dst + o + 256) = make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
+    }
+}
+
 }  // namespace
+
+// Which k = 128 bitsliced kernel (CDA_RS8_BS = 1: 4 codewords per workgroup,
+// 2: the half-footprint variant; A/B knob).
+static int rs8_variant() {
+    static const int v = [] {
+        const char* e = getenv("CDA_RS8_BS");
+        return e ? atoi(e) : 2;
+    }();
+    return v;
+}
 
 // Bitsliced path for k = 128 codewords of 512-B shards (segments of the job
 // must hold a multiple of 4 codewords).
 hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
+    if (rs8_variant() == 2) {
+        if (j.seg[0].n_cw % 2 || (j.n_seg > 1 && j.seg[1].n_cw % 2)) return hipErrorInvalidValue;
+        const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
+        hipLaunchKernelGGL(rs8_bs_half_kernel, dim3(ncw / 2, n), dim3(512), kHalfLdsBytes, s, j);
+        return hipGetLastError();
+    }
     const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
     if (j.seg[0].n_cw % 4 || (j.n_seg > 1 && j.seg[1].n_cw % 4)) return hipErrorInvalidValue;
     static bool attr = false;

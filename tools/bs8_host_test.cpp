@@ -84,6 +84,60 @@ int main() {
         }
     }
     if (got != expect) { printf("encode FAIL\n"); return 1; }
+
+    // half layout (rs8_bs_half_kernel): lane (u, h) holds shards 16u + 2j + h in
+    // H[u][h][8j + p]; the d = 1 steps see the partner lane's planes as P
+    uint32_t H[8][2][64];
+    const uint32_t hm[2] = {0xFFFFFFFFu, 0u};
+    auto cross = [&](int u, int j, auto step) {   // both lanes read the other's pre-step planes
+        uint32_t P0[8], P1[8];
+        memcpy(P0, &H[u][1][8 * j], 32);
+        memcpy(P1, &H[u][0][8 * j], 32);
+        step(&H[u][0][8 * j], P0, hm[0]);
+        step(&H[u][1][8 * j], P1, hm[1]);
+    };
+    for (int u = 0; u < 8; u++) {
+        for (int h = 0; h < 2; h++)
+            for (int j = 0; j < 8; j++) {
+                memcpy(&H[u][h][8 * j], &data[(16 * u + 2 * j + h) * 32], 32);
+                transpose8(&H[u][h][8 * j]);
+            }
+        with_u(u, [&](auto U) {
+            constexpr int UU = decltype(U)::value;
+            sfor<0, 8, 1>([&](auto jj) {
+                constexpr int j = decltype(jj)::value;
+                cross(u, j, [](uint32_t* x, const uint32_t* P, uint32_t h0) { ifft_d1<ifft_d1_log<UU>(j)>(x, P, h0); });
+            });
+            for (int h = 0; h < 2; h++) pass_a_hi<UU>(H[u][h]);
+        });
+    }
+    // A -> B: lane (w, h) gets shards 16u + 2w + h of every u in R[8u + p]
+    uint32_t HB[8][2][64];
+    for (int w = 0; w < 8; w++)
+        for (int h = 0; h < 2; h++) {
+            for (int u = 0; u < 8; u++) memcpy(&HB[w][h][8 * u], &H[u][h][8 * w], 32);
+            pass_b(HB[w][h]);
+        }
+    for (int w = 0; w < 8; w++)
+        for (int h = 0; h < 2; h++)
+            for (int u = 0; u < 8; u++) memcpy(&H[u][h][8 * w], &HB[w][h][8 * u], 32);
+    std::vector<uint8_t> got2(K * 32);
+    for (int u = 0; u < 8; u++) {
+        with_u(u, [&](auto U) {
+            constexpr int UU = decltype(U)::value;
+            for (int h = 0; h < 2; h++) pass_c_hi<UU>(H[u][h]);
+            sfor<0, 8, 1>([&](auto jj) {
+                constexpr int j = decltype(jj)::value;
+                cross(u, j, [](uint32_t* x, const uint32_t* P, uint32_t h0) { fft_d1<fft_d1_log<UU>(j)>(x, P, h0); });
+            });
+        });
+        for (int h = 0; h < 2; h++)
+            for (int j = 0; j < 8; j++) {
+                transpose8(&H[u][h][8 * j]);
+                memcpy(&got2[(16 * u + 2 * j + h) * 32], &H[u][h][8 * j], 32);
+            }
+    }
+    if (got2 != expect) { printf("half-layout encode FAIL\n"); return 1; }
     printf("bs8 host test OK\n");
     return 0;
 }
