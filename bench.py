@@ -189,14 +189,20 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def stage_report(st: dict, k: int, batch: int, inplace: bool = False) -> dict:
+def stage_report(st: dict, k: int, batch: int, inplace: bool = False, steps: int = 0) -> dict:
+    """Per-stage roofline records.  With `steps` (> 0) the stage may run as
+    several launches per step (the chunked batch pipeline): `avg_ms` is then
+    the stage's time per step and the work is the whole batch's; otherwise one
+    launch covers `batch` squares."""
     out = {}
     comp = compressions(k)
     for name, (ms, n) in st.items():
         if n == 0:
             continue
-        avg = ms / n
+        avg = ms / (steps if steps > 0 else n)
         rec = {"avg_ms": avg, "launches": n}
+        if steps > 0:
+            rec["launches_per_step"] = n / steps
         if name in comp:
             c = comp[name] * batch
             rec.update(bound="valu", achieved=c * SHA_SLOTS / (avg * 1e-3) / 1e12, peak=PEAK_VALU_TOPS,
@@ -710,7 +716,7 @@ def main():
 
     total_sq = B * world * args.steps
     value = total_sq / el
-    stages = stage_report(st, k, B, args.layout == "inplace")
+    stages = stage_report(st, k, B, args.layout == "inplace", n_prof)
     dom = max((s for s in stages if "achieved" in stages[s]), key=lambda s: stages[s]["avg_ms"])
     d = stages[dom]
     roofline = {"bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"], "unit": d["unit"],

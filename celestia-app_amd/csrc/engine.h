@@ -218,13 +218,18 @@ class Engine {
     static void copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds);
     hipEvent_t order_ev_ = nullptr;   // end of the last call's GPU work
     bool order_used_ = false;
-    // Batch pipeline: RS of chunk i+1 (HBM/VALU mix) overlaps the SHA-256
-    // stages of chunk i (VALU) on a second stream.
-    hipStream_t rs_stream_ = nullptr, hash_stream_ = nullptr;
-    bool cu_split_ = false;   // CDA_RS_CU: RS and hash streams on disjoint CU masks
+    // Batch pipeline: RS of chunk i+1 (memory-bound) runs on rs_stream_ under
+    // the SHA-256 of chunk i (VALU-bound) on the caller's stream.
+    hipStream_t rs_stream_ = nullptr;
     std::vector<hipEvent_t> sync_events_;
     uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
     hipEvent_t sync_event(size_t i);
+    int dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s);
+    void dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]);
+    int dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
+                  const Forest (&f)[2], Forest (&post)[2], hipStream_t s);
+    int dah_finish(uint32_t k, uint32_t n, uint32_t from, Forest (&f)[2], uint8_t* d_roots, uint32_t* d_err,
+                   int32_t* d_status, hipStream_t s);
     int enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                                   uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
                                   hipStream_t s);

@@ -71,7 +71,6 @@ Engine::~Engine() {
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (rs_stream_) (void)hipStreamDestroy(rs_stream_);
-    if (hash_stream_) (void)hipStreamDestroy(hash_stream_);
 }
 
 int Engine::check(hipError_t e, const char* what) {
@@ -97,46 +96,13 @@ int Engine::init() {
     if ((rc = check(hipEventCreateWithFlags(&ev_rs_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     if ((rc = check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
-    // lower value is a higher priority), so RS workgroups win free CU slots.
-    // CDA_RS_CU=S:R[:G] (tuning): spatial split of the pipeline's streams.  CU
-    // mask bit i goes to the RS stream when (i / G) % S < R (G defaults to 8,
-    // so the split is even whether the driver stripes mask bits over the 8
-    // XCDs or numbers each XCD's CUs contiguously); the hash stream gets the
-    // complement unless CDA_HASH_ALL_CUS=1.  RS is HBM/latency-bound with one
-    // workgroup per CU, SHA-256 VALU-bound: on disjoint CUs they co-run without
-    // fighting over one CU's VGPRs and LDS.
-    const char* cu_env = getenv("CDA_RS_CU");
-    if (cu_env) {
-        unsigned S = 8, R = 1, G = 8;
-        if (sscanf(cu_env, "%u:%u:%u", &S, &R, &G) < 2 || S == 0 || G == 0 || R >= S)
-            return fail(CDA_ERR_INVALID, "CDA_RS_CU must be S:R[:G] with 0 < R < S");
-        int ncu = 0;
-        if ((rc = check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_),
-                        "hipDeviceGetAttribute")))
-            return rc;
-        const uint32_t words = (uint32_t)(ncu + 31) / 32;
-        std::vector<uint32_t> rs_mask(words, 0), hash_mask(words, 0);
-        for (int i = 0; i < ncu; i++) {
-            const bool rs = (i / G) % S < R;
-            (rs ? rs_mask : hash_mask)[i / 32] |= 1u << (i % 32);
-        }
-        if (getenv("CDA_HASH_ALL_CUS"))
-            for (int i = 0; i < ncu; i++) hash_mask[i / 32] |= 1u << (i % 32);
-        if ((rc = check(hipExtStreamCreateWithCUMask(&rs_stream_, words, rs_mask.data()), "hipExtStreamCreateWithCUMask")))
-            return rc;
-        if ((rc = check(hipExtStreamCreateWithCUMask(&hash_stream_, words, hash_mask.data()),
-                        "hipExtStreamCreateWithCUMask")))
-            return rc;
-        cu_split_ = true;
-    } else if (const char* env = getenv("CDA_RS_PRIORITY")) {
+    // lower value is a higher priority).
+    if (const char* env = getenv("CDA_RS_PRIORITY")) {
         if ((rc = check(hipStreamCreateWithPriority(&rs_stream_, hipStreamNonBlocking, atoi(env)), "hipStreamCreate")))
             return rc;
     } else if ((rc = check(hipStreamCreateWithFlags(&rs_stream_, hipStreamNonBlocking), "hipStreamCreate"))) {
         return rc;
     }
-    if (!hash_stream_ &&
-        (rc = check(hipStreamCreateWithFlags(&hash_stream_, hipStreamNonBlocking), "hipStreamCreate")))
-        return rc;
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
@@ -302,42 +268,96 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
     return CDA_OK;
 }
 
-int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols,
-                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s) {
-    if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
-    const uint32_t W = 2 * k;
+// enqueue_dah in pieces.  The serial path runs them back to back; the batch
+// pipeline (enqueue_extend_dah) hashes each chunk as soon as its RS is done
+// (dah_chunk) and runs the latency-bound rest once for the whole batch
+// (dah_finish).
+int Engine::dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s) {
     const uint64_t slots_sq = (uint64_t)W * W * kSlot;
     int rc;
     if ((rc = check(leaf_.ensure(slots_sq * n), "hipMalloc leaf slots"))) return rc;
     if ((rc = check(lvl_.ensure(slots_sq * n), "hipMalloc level slots"))) return rc;
     if ((rc = check(root_slots_.ensure((size_t)n * 2 * W * kSlot), "hipMalloc root slots"))) return rc;
-    if ((rc = check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync"))) return rc;
-    mark_begin(kStageLeaves, s);
-    const CellGrid g{d_eds, (uint64_t)W * W * kShare, W, W, W, 0, 0, k};
-    if ((rc = check(launch_leaves(g, n, leaf_.as<uint8_t>(), d_err, true, true, s), "leaf hashing"))) return rc;
-    mark_end(s);
-    mark_begin(kStageLevels, s);
-    // row trees: leaves (t, i); column trees: leaves (i, t) of the same leaf grid
-    Forest f[2]{};
-    // roots go packed to d_rows / d_cols and as 96-B slots (rows then
-    // columns) to root_slots_ for the data root
+    if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
+    return check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync");
+}
+
+// Row trees: leaves (t, i); column trees: leaves (i, t) of the same leaf grid.
+// Roots go packed to d_rows / d_cols and as 96-B slots (rows then columns) to
+// root_slots_ for the data root.
+void Engine::dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]) {
+    const uint64_t slots_sq = (uint64_t)W * W * kSlot;
     f[0] = Forest{leaf_.as<uint8_t>(), slots_sq, W, W, 1, nullptr, 0, d_rows, (uint64_t)W * kNode,
                   root_slots_.as<uint8_t>(), (uint64_t)2 * W * kSlot, 0};
     f[1] = Forest{leaf_.as<uint8_t>(), slots_sq, W, 1, W, nullptr, 0, d_cols, (uint64_t)W * kNode,
                   root_slots_.as<uint8_t>(), (uint64_t)2 * W * kSlot, W};
-    const uint64_t off[2] = {0, slots_sq / 2};
+}
+
+// Leaves and the NMT levels down to `stop` nodes per tree of squares
+// [i0, i0 + m).  f: the batch's forests from dah_forests; on return `post`
+// describes (for the whole batch) the level the chunk stopped at.
+int Engine::dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
+                      const Forest (&f)[2], Forest (&post)[2], hipStream_t s) {
+    const uint32_t W = 2 * k;
+    const uint64_t slots_sq = (uint64_t)W * W * kSlot, eds_sq = (uint64_t)W * W * kShare;
+    int rc;
+    mark_begin(kStageLeaves, s);
+    const CellGrid g{d_eds + i0 * eds_sq, eds_sq, W, W, W, 0, 0, k};
+    if ((rc = check(launch_leaves(g, m, leaf_.as<uint8_t>() + i0 * slots_sq, d_err + i0, true, true, s),
+                    "leaf hashing")))
+        return rc;
+    mark_end(s);
+    Forest fc[2] = {f[0], f[1]};
+    for (int i = 0; i < 2; i++) {
+        fc[i].in += i0 * fc[i].in_sq;
+        if (fc[i].roots) fc[i].roots += i0 * fc[i].roots_sq;
+        if (fc[i].root_slots) fc[i].root_slots += i0 * fc[i].rslot_sq;
+    }
+    if (W > stop) {
+        mark_begin(kStageLevels, s);
+        const uint64_t off[2] = {0, slots_sq / 2};
+        if ((rc = run_forests(fc, 2, W, m, lvl_.as<uint8_t>() + i0 * slots_sq, leaf_.as<uint8_t>() + i0 * slots_sq,
+                              slots_sq, off, s, stop)))
+            return rc;
+        mark_end(s);
+    }
+    for (int i = 0; i < 2; i++) {
+        post[i] = fc[i];
+        post[i].in -= i0 * fc[i].in_sq;
+        post[i].roots = f[i].roots;
+        post[i].root_slots = f[i].root_slots;
+    }
+    return CDA_OK;
+}
+
+// The levels below `from` nodes per tree (f = dah_chunk's post), the fused
+// tree top and the data root (which also writes d_status), for all n squares.
+int Engine::dah_finish(uint32_t k, uint32_t n, uint32_t from, Forest (&f)[2], uint8_t* d_roots, uint32_t* d_err,
+                       int32_t* d_status, hipStream_t s) {
+    const uint32_t W = 2 * k;
+    const uint64_t slots_sq = (uint64_t)W * W * kSlot;
+    int rc;
     // Wide per-level launches while a level has at least a wave per SIMD of
     // parents; the latency-bound rest of the trees (and the data root's RFC
     // leaf digests) in one tree_top_kernel launch.
-    const uint32_t top = top_fuse_nodes(W, n);
-    if ((rc = run_forests(f, 2, W, n, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), slots_sq, off, s, top))) return rc;
-    if (top) {
-        if (d_roots && (rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
-        if ((rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig_.as<uint32_t>() : nullptr, 2 * W, s),
-                        "nmt tree top")))
+    uint32_t top = top_fuse_nodes(W, n);
+    if (top > from) top = from;
+    if (from > 1) {
+        const uint32_t stop = top ? top : 1;
+        mark_begin(kStageLevels, s);
+        if (from > stop) {
+            // the chunks ran ctz(W) - ctz(from) levels, the first into lvl_
+            const bool in_lvl = ((__builtin_ctz(W) - __builtin_ctz(from)) & 1) != 0;
+            uint8_t* a = in_lvl ? leaf_.as<uint8_t>() : lvl_.as<uint8_t>();
+            uint8_t* b = in_lvl ? lvl_.as<uint8_t>() : leaf_.as<uint8_t>();
+            const uint64_t off[2] = {0, slots_sq / 2};
+            if ((rc = run_forests(f, 2, from, n, a, b, slots_sq, off, s, stop))) return rc;
+        }
+        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig_.as<uint32_t>() : nullptr, 2 * W, s),
+                               "nmt tree top")))
             return rc;
+        mark_end(s);
     }
-    mark_end(s);
     // the data-root launch also writes the per-square push-order status
     if (d_roots && top) {
         mark_begin(kStageDataRoot, s);
@@ -347,7 +367,6 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
         mark_end(s);
     } else if (d_roots) {   // NULL: roots only (repair verification needs no data root)
         mark_begin(kStageDataRoot, s);
-        if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
         if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s,
                                                d_err, d_status),
                         "data root")))
@@ -356,6 +375,20 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     }
     if (!d_roots && d_status && (rc = check(launch_status(d_err, n, d_status, s), "status"))) return rc;
     return CDA_OK;
+}
+
+int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols,
+                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s) {
+    if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
+    const uint32_t W = 2 * k;
+    int rc;
+    if ((rc = dah_prepare(W, n, d_err, s))) return rc;
+    Forest f[2], post[2];
+    dah_forests(W, d_rows, d_cols, f);
+    const uint32_t top = top_fuse_nodes(W, n);
+    const uint32_t stop = top ? top : 1;
+    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) return rc;
+    return dah_finish(k, n, stop, post, d_roots, d_err, d_status, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -449,53 +482,58 @@ hipEvent_t Engine::sync_event(size_t i) {
 }
 
 // Batch pipeline.  The batch is cut into chunks of c squares; chunk i's RS
-// extension runs on rs_stream_, its roots on hash_stream_ after an event, so
-// the RS of chunk i+1 (memory-heavy) overlaps the SHA-256 of chunk i
-// (VALU-bound).  Both internal streams start after the work already queued on
-// the caller's stream `s`, and `s` waits for both at the end, so the call keeps
-// single-stream semantics for the caller.  Events are re-recorded by later
-// calls only after hipStreamWaitEvent has captured them (HIP semantics).
+// extension runs on rs_stream_ and its leaves and wide NMT levels on the
+// caller's stream after an event, so the RS of chunk i+1 (memory-bound: its
+// half-footprint kernel leaves room for hash waves on every CU) runs under the
+// SHA-256 of chunk i (VALU-bound).  The narrow levels, the tree tops and the
+// data roots -- latency-bound -- run once for the whole batch at the end.
+// rs_stream_ starts after the work already queued on `s` and `s` waits for
+// every chunk's RS before hashing it, so the call keeps single-stream
+// semantics for the caller.  Events are re-recorded by later calls only after
+// hipStreamWaitEvent has captured them (HIP semantics).
 int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                                uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
                                hipStream_t s) {
     if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
-    // Default serial: measured on MI355X (profiles/r01_pipeline_sweep.txt) the
-    // v_perm GF(2^8) encoder is VALU-bound like SHA-256, so co-running them
-    // only shares the SIMDs (and per-chunk level/data-root tails cost extra).
-    uint32_t c = pipeline_chunk_ ? pipeline_chunk_ : n;
+    const uint32_t c = pipeline_chunk_ ? pipeline_chunk_ : n;
     if (c >= n) return enqueue_extend_dah_serial(d_ods, k, n, d_eds, d_rows, d_cols, d_roots, d_err, d_status, s);
     const uint32_t W = 2 * k;
     const uint64_t ods_sq = (uint64_t)k * k * kShare, eds_sq = (uint64_t)W * W * kShare;
     const uint32_t n_chunks = (n + c - 1) / c;
+    // per chunk: the levels whose parents (over the chunk's 2W trees) fill at
+    // least a wave per SIMD (1024 SIMDs x 64 lanes)
+    uint32_t stop = 1;
+    for (uint32_t m = W; m >= 2; m /= 2)
+        if ((uint64_t)c * 2 * W * (m / 2) < 65536) {
+            stop = m;
+            break;
+        }
     int rc;
     hipEvent_t start = sync_event(0);
-    if (!start || !sync_event(n_chunks + 2)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
+    if (!start || !sync_event(n_chunks)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
+    if ((rc = dah_prepare(W, n, d_err, s))) return rc;
     if ((rc = check(hipEventRecord(start, s), "hipEventRecord"))) return rc;
     if ((rc = check(hipStreamWaitEvent(rs_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
-    if ((rc = check(hipStreamWaitEvent(hash_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
     for (uint32_t i = 0; i < n_chunks; i++) {
         const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
-        uint8_t* eds = d_eds + i0 * eds_sq;
-        // With a CU split the first chunk's RS runs on the hash stream's CUs
-        // (they have nothing else to do yet) instead of the small RS subset.
-        if (i == 0 && cu_split_) {
-            if ((rc = enqueue_extend(d_ods, k, m, eds, hash_stream_))) return rc;
-        } else {
-            if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, eds, rs_stream_))) return rc;
-            hipEvent_t ev = sync_event(1 + i);
-            if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
-            if ((rc = check(hipStreamWaitEvent(hash_stream_, ev, 0), "hipStreamWaitEvent"))) return rc;
-        }
-        if ((rc = enqueue_dah(eds, k, m, d_rows + (size_t)i0 * W * kNode, d_cols + (size_t)i0 * W * kNode,
-                              d_roots + (size_t)i0 * 32, d_err + i0, d_status ? d_status + i0 : nullptr,
-                              hash_stream_)))
+        if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, d_eds + i0 * eds_sq, rs_stream_)))
             return rc;
+        hipEvent_t ev = sync_event(1 + i);
+        if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
     }
-    hipEvent_t done = sync_event(1 + n_chunks);
-    if ((rc = check(hipEventRecord(done, hash_stream_), "hipEventRecord"))) return rc;
-    if ((rc = check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent"))) return rc;
-    // rs_stream_ work all precedes `done` through the per-chunk events.
-    return CDA_OK;
+    Forest f[2], post[2];
+    dah_forests(W, d_rows, d_cols, f);
+    for (uint32_t i = 0; i < n_chunks; i++) {
+        const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
+        if ((rc = check(hipStreamWaitEvent(s, sync_event(1 + i), 0), "hipStreamWaitEvent"))) return rc;
+        Forest p[2];
+        if ((rc = dah_chunk(d_eds, k, i0, m, stop, d_err, f, p, s))) return rc;
+        if (i == 0) {
+            post[0] = p[0];
+            post[1] = p[1];
+        }
+    }
+    return dah_finish(k, n, stop, post, d_roots, d_err, d_status, s);
 }
 
 int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n,

@@ -105,11 +105,12 @@ __device__ __forceinline__ void load_raw16(const uint4* p, uint32_t (&w)[16]) {
 // Big-endian message word from share bytes 4j+2 .. 4j+5 (raw words j, j+1).
 __device__ __forceinline__ uint32_t body_word(uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x02030405u); }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEAF_WAVES))) void leaf_kernel(const CellGrid g, uint8_t* __restrict__ slots,
-                                                  uint32_t* __restrict__ err, int check_rows, int check_cols) {
-    const uint32_t cell = blockIdx.x * 256 + threadIdx.x;
+// One virtual block (bx = 256-cell group, by = square) of the leaf launch.
+__device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restrict__ slots, uint32_t* __restrict__ err,
+                                           int check_rows, int check_cols, uint32_t bx, uint32_t by) {
+    const uint32_t cell = bx * 256 + threadIdx.x;
     if (cell >= g.rows * g.cols) return;
-    const size_t sq = blockIdx.y;
+    const size_t sq = by;
     const uint32_t r = cell / g.cols, c = cell % g.cols;
     const uint32_t gr = g.row0 + r, gc = g.col0 + c, k = g.k;
     const bool parity = !(gr < k && gc < k);
@@ -197,6 +198,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEAF_WA
     }
 }
 
+// The hash launches run a 1-D grid over virtual blocks b = by * nbx + bx: one
+// block per workgroup when the grid covers them all, or a capped persistent
+// grid (CDA_HASH_WG_PER_CU workgroups per CU) whose workgroups stride over
+// them -- then the hash kernels hold a fixed share of every CU and leave room
+// for the batch pipeline's RS workgroups (engine.hip enqueue_extend_dah).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEAF_WAVES))) void leaf_kernel(
+    const CellGrid g, uint8_t* __restrict__ slots, uint32_t* __restrict__ err, int check_rows, int check_cols,
+    uint32_t nbx, uint32_t nblocks) {
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+        leaf_block(g, slots, err, check_rows, check_cols, b % nbx, b / nbx);
+}
+
 // ---------------------------------------------------------------------------
 // One NMT level of up to two forests (blockIdx.z).  Thread -> (tree, parent):
 // parents of one tree are adjacent threads when nodes are adjacent slots
@@ -241,12 +254,13 @@ __device__ __forceinline__ void hash_node(const uint32_t (&L)[kSlotWords], const
     inner_node_words(L, R, st.h, o);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_WAVES))) void level_kernel(const Forest2 fs, uint32_t n_in) {
-    const Forest& F = fs.f[blockIdx.z];
+// One virtual block (bx = 256-parent group, by = square, bz = forest).
+__device__ __forceinline__ void level_block(const Forest2& fs, uint32_t n_in, uint32_t bx, uint32_t by, uint32_t bz) {
+    const Forest& F = fs.f[bz];
     const uint32_t n_out = n_in / 2;
-    const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t idx = bx * 256 + threadIdx.x;
     if (idx >= F.n_trees * n_out) return;
-    const size_t sq = blockIdx.y;
+    const size_t sq = by;
     uint32_t t, p;
     if (F.node_stride == 1) {
         // all trees' left-half parents first, then the right halves: a wave
@@ -280,6 +294,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
         if (F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
     } else {
         store_slot(F.out + sq * F.out_sq + ((size_t)t * n_out + p) * kSlot, o);
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_WAVES))) void level_kernel(
+    const Forest2 fs, uint32_t n_in, uint32_t nbx, uint32_t nsq, uint32_t nblocks) {
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint32_t bx = b % nbx, r = b / nbx;
+        level_block(fs, n_in, bx, r % nsq, r / nsq);
     }
 }
 
@@ -527,11 +549,29 @@ static size_t hash_lds(const void* fn) {
     return v > 0 ? (size_t)v : 0;
 }
 
+// Workgroups of a hash launch over `nblocks` virtual blocks: all of them, or
+// CDA_HASH_WG_PER_CU x the device's CUs (persistent; tuning / batch pipeline).
+static uint32_t hash_grid(uint32_t nblocks) {
+    static const uint32_t cap = [] {
+        const char* e = getenv("CDA_HASH_WG_PER_CU");
+        const int per = e ? atoi(e) : 0;
+        if (per <= 0) return 0u;
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return 0u;
+        return (uint32_t)(per * cus);
+    }();
+    return cap && nblocks > cap ? cap : nblocks;
+}
+
 hipError_t launch_leaves(const CellGrid& g, uint32_t n, uint8_t* slots, uint32_t* err, bool check_rows,
                          bool check_cols, hipStream_t s) {
-    dim3 grid((g.rows * g.cols + 255) / 256, n);
-    hipLaunchKernelGGL(leaf_kernel, grid, dim3(256), hash_lds(reinterpret_cast<const void*>(leaf_kernel)), s, g,
-                       slots, err, check_rows ? 1 : 0, check_cols ? 1 : 0);
+    const uint32_t nbx = (g.rows * g.cols + 255) / 256, nblocks = nbx * n;
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(leaf_kernel, dim3(hash_grid(nblocks)), dim3(256),
+                       hash_lds(reinterpret_cast<const void*>(leaf_kernel)), s, g, slots, err, check_rows ? 1 : 0,
+                       check_cols ? 1 : 0, nbx, nblocks);
     return hipGetLastError();
 }
 
@@ -543,9 +583,10 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
         fs.f[i] = f[i];
         maxw = maxw > f[i].n_trees * (n_in / 2) ? maxw : f[i].n_trees * (n_in / 2);
     }
-    dim3 grid((maxw + 255) / 256, n, n_forest);
-    hipLaunchKernelGGL(level_kernel, grid, dim3(256), hash_lds(reinterpret_cast<const void*>(level_kernel)), s, fs,
-                       n_in);
+    const uint32_t nbx = (maxw + 255) / 256, nblocks = nbx * n * n_forest;
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(level_kernel, dim3(hash_grid(nblocks)), dim3(256),
+                       hash_lds(reinterpret_cast<const void*>(level_kernel)), s, fs, n_in, nbx, n, nblocks);
     return hipGetLastError();
 }
 

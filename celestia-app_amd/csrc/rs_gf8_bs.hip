@@ -293,7 +293,21 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
     if (rs8_variant() == 2) {
         if (j.seg[0].n_cw % 2 || (j.n_seg > 1 && j.seg[1].n_cw % 2)) return hipErrorInvalidValue;
         const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
-        hipLaunchKernelGGL(rs8_bs_half_kernel, dim3(ncw / 2, n), dim3(512), kHalfLdsBytes, s, j);
+        // CDA_RS8_LDS (tuning): LDS reserved per workgroup, >= 64 KiB; above
+        // 80 KiB one workgroup per CU, leaving VGPRs for co-running hash waves
+        static const uint32_t lds = [] {
+            const char* e = getenv("CDA_RS8_LDS");
+            const uint32_t v = e ? (uint32_t)atoi(e) : 0;
+            return v > kHalfLdsBytes && v <= 160 * 1024 ? v : kHalfLdsBytes;
+        }();
+        static bool attr = false;
+        if (lds > 64 * 1024 && !attr) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs8_bs_half_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL(rs8_bs_half_kernel, dim3(ncw / 2, n), dim3(512), lds, s, j);
         return hipGetLastError();
     }
     const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);

@@ -1,8 +1,9 @@
-"""Two-stream batch pipeline (engine.hip enqueue_extend_dah): chunked RS on
-one stream, NMT / data root on another, optionally on disjoint CU masks
-(CDA_RS_CU).  Tuning knobs read at context creation; every setting must give
-the serial path's bytes (and the serial path is pinned to the oracle by
-test_gpu_parity.py)."""
+"""Batch pipeline (engine.hip enqueue_extend_dah): each chunk's RS on an
+internal stream, its leaves and wide NMT levels on the caller's stream after
+an event, and the narrow levels, tree tops and data roots once for the whole
+batch (dah_finish).  Tuning knobs are read at context creation; every setting
+must give the serial path's bytes (and the serial path is pinned to the oracle
+by test_gpu_parity.py)."""
 import os
 
 import numpy as np
@@ -29,9 +30,12 @@ def _ctx_with(env):
 
 @pytest.mark.parametrize("k,n,env", [
     (16, 6, {"CDA_PIPELINE_CHUNK": "2"}),
-    (16, 6, {"CDA_PIPELINE_CHUNK": "2", "CDA_RS_CU": "8:1"}),
-    (128, 3, {"CDA_PIPELINE_CHUNK": "1", "CDA_RS_CU": "16:3"}),
-    (128, 3, {"CDA_PIPELINE_CHUNK": "2", "CDA_RS_CU": "8:1:1", "CDA_HASH_ALL_CUS": "1"}),
+    (16, 5, {"CDA_PIPELINE_CHUNK": "2"}),                     # ragged last chunk
+    (128, 3, {"CDA_PIPELINE_CHUNK": "1"}),
+    (128, 6, {"CDA_PIPELINE_CHUNK": "4"}),                    # 4 + 2
+    (128, 4, {"CDA_PIPELINE_CHUNK": "2", "CDA_RS8_LDS": "98304"}),
+    (128, 4, {"CDA_PIPELINE_CHUNK": "2", "CDA_RS_PRIORITY": "-1"}),
+    (64, 8, {"CDA_PIPELINE_CHUNK": "3"}),
 ])
 def test_pipeline_matches_serial(ctx, k, n, env):
     ods = np.stack([coracle.random_square(k, i) for i in range(n)])
@@ -47,6 +51,21 @@ def test_pipeline_matches_serial(ctx, k, n, env):
     assert bytes(got[3][-1]) == e_root
 
 
-def test_bad_cu_split_fails_loudly():
-    with pytest.raises(_lib.CdaError):
-        _ctx_with({"CDA_RS_CU": "8:9"})
+def test_pipeline_push_order_status_per_square():
+    """A namespace-order violation in one square of a later chunk is reported
+    for that square only (the push-order words are filled once per batch and
+    the status written by the batch's data-root launch)."""
+    k, n = 32, 5
+    ods = np.stack([coracle.random_square(k, i) for i in range(n)])
+    bad = ods[3].reshape(k, k, 512)
+    bad[2, 5, :29], bad[2, 6, :29] = bad[2, 6, :29].copy(), bad[2, 5, :29].copy()
+    if bytes(bad[2, 5, :29]) == bytes(bad[2, 6, :29]):
+        pytest.skip("equal namespaces")
+    pc = _ctx_with({"CDA_PIPELINE_CHUNK": "2"})
+    try:
+        _, _, _, roots, status = da.extend_dah_batch(ods, ctx=pc)
+        ref = da.extend_dah_batch(ods, ctx=None)
+    finally:
+        pc.close()
+    assert list(status != 0) == [False, False, False, True, False]
+    assert np.array_equal(roots[[0, 1, 2, 4]], ref[3][[0, 1, 2, 4]])
