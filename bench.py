@@ -39,6 +39,7 @@ SHA_SLOTS = 2182
 # profiles/r01f_valu_probe.txt "alignbit+xor"); HBM 6.29 TB/s float4 copy
 # (MI355X_MICROARCH.md).  Reported beside the spec peak as `achievable`.
 ACHIEVABLE_SHA_COMP_S = 28.453e9
+CONFIG5_TIMEOUT_S = float(os.environ.get("CDA_CONFIG5_TIMEOUT_S", "180"))
 ACHIEVABLE_VALU_TOPS = ACHIEVABLE_SHA_COMP_S * SHA_SLOTS / 1e12
 ACHIEVABLE_HBM_GBS = 6290.0
 SHARE = 512
@@ -860,21 +861,8 @@ def main():
         extras["k512"]["batch2"] = {"squares_per_s": n5 * nb / elb, "ms_per_square": 1e3 * elb / (n5 * nb)}
         del eb
 
-    if (world > 1 or args.config5) and not args.no_extras:
-        # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
-        # all-to-all of the row-encoded blocks, column encode + hashing per
-        # rank, gather of subtree/column roots, combine on rank 0).
-        try:
-            extras["config5"] = config5(ctx, dev, rank, world, 512)
-        except Exception as e:  # report, never lose the headline line
-            extras["config5"] = {"error": f"{type(e).__name__}: {e}"}
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
-        cpu = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
-
-    if rank == 0:
-        line = {
+    def make_line(cpu):
+        return {
             "metric": "EDS+DAH squares/sec (k=128)",
             "value": value,
             "unit": "squares/s",
@@ -904,7 +892,37 @@ def main():
             "cpu_baseline": cpu,
             "extras": extras,
         }
-        print(json.dumps(line))
+
+    if (world > 1 or args.config5) and not args.no_extras:
+        # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
+        # all-to-all of the row-encoded blocks, column encode + hashing per
+        # rank, gather of subtree/column roots, combine on rank 0).  A
+        # collective that never returns must not cost the headline line: a
+        # watchdog prints it (rank 0) and ends every rank cleanly.
+        import threading
+
+        def on_timeout():
+            extras["config5"] = {"error": f"no result after {CONFIG5_TIMEOUT_S} s (collective hang?)"}
+            if rank == 0:
+                print(json.dumps(make_line(None)), flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(CONFIG5_TIMEOUT_S, on_timeout)
+        wd.daemon = True
+        wd.start()
+        try:
+            extras["config5"] = config5(ctx, dev, rank, world, 512)
+        except Exception as e:  # report, never lose the headline line
+            extras["config5"] = {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            wd.cancel()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
+        cpu = cpu_baseline(k, args.cpu_seconds, args.cpu_threads)
+
+    if rank == 0:
+        print(json.dumps(make_line(cpu)))
     if dist.is_initialized():
         dist.destroy_process_group()
 
