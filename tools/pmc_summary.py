@@ -17,7 +17,7 @@ import sys
 
 STAGE = {"rfc_leaf_kernel": "data_root_leaves", "data_root_digest_kernel": "data_root_digest",
          "leaf_kernel": "nmt_leaves", "level_kernel": "nmt_levels", "data_root_kernel": "data_root",
-         "rs8_bs_kernel": "rs_gf8_bs", "rs8_job_kernel": "rs_gf8", "rs8_flat_kernel": "rs_gf8_flat", "rs16_cw_kernel": "rs_gf16", "rs16_lds_kernel": "rs_gf16_lds",
+         "rs8_bs_half_kernel": "rs_gf8_bs", "rs8_bs_kernel": "rs_gf8_bs", "rs8_job_kernel": "rs_gf8", "rs8_flat_kernel": "rs_gf8_flat", "rs16_cw_kernel": "rs_gf16", "rs16_lds_kernel": "rs_gf16_lds",
          "order_kernel": "order_check"}
 
 
