@@ -885,7 +885,9 @@ def main():
             "ods_gb_per_s": value * k * k * SHARE / 1e9,
             "stage_pass": {"steps": n_prof, "ms_per_step": 1e3 * el_prof / n_prof,
                            "note": "stages and rooflines come from this separate pass with HIP events at every "
-                                   "stage border; value / ms_per_step come from the event-free timed region"},
+                                   "stage border, on the one-stream schedule (with profiling on the library "
+                                   "does not split the hash stages over two streams); value / ms_per_step come "
+                                   "from the event-free timed region with the default two-stream hash split"},
             "roofline": roofline,
             "rs_roofline": rs_roof,
             "stages": stages,

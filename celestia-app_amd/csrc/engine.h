@@ -218,11 +218,12 @@ class Engine {
     static void copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds);
     hipEvent_t order_ev_ = nullptr;   // end of the last call's GPU work
     bool order_used_ = false;
-    // Batch pipeline: RS of chunk i+1 (memory-bound) runs on rs_stream_ under
-    // the SHA-256 of chunk i (VALU-bound) on the caller's stream.
-    hipStream_t rs_stream_ = nullptr;
+    // Second stream of a call: half of a batch's hash stages (enqueue_dah), or
+    // the batch pipeline's RS chunks (enqueue_extend_dah, CDA_PIPELINE_CHUNK).
+    hipStream_t aux_stream_ = nullptr;
     std::vector<hipEvent_t> sync_events_;
     uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
+    uint32_t hash_split_ = 2;       // CDA_HASH_SPLIT: hash the batch as two halves on two streams (0/1 = off)
     hipEvent_t sync_event(size_t i);
     int dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s);
     void dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]);

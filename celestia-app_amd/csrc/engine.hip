@@ -70,7 +70,7 @@ Engine::~Engine() {
     if (ev_out_) (void)hipEventDestroy(ev_out_);
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
-    if (rs_stream_) (void)hipStreamDestroy(rs_stream_);
+    if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
 }
 
 int Engine::check(hipError_t e, const char* what) {
@@ -98,12 +98,13 @@ int Engine::init() {
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority).
     if (const char* env = getenv("CDA_RS_PRIORITY")) {
-        if ((rc = check(hipStreamCreateWithPriority(&rs_stream_, hipStreamNonBlocking, atoi(env)), "hipStreamCreate")))
+        if ((rc = check(hipStreamCreateWithPriority(&aux_stream_, hipStreamNonBlocking, atoi(env)), "hipStreamCreate")))
             return rc;
-    } else if ((rc = check(hipStreamCreateWithFlags(&rs_stream_, hipStreamNonBlocking), "hipStreamCreate"))) {
+    } else if ((rc = check(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking), "hipStreamCreate"))) {
         return rc;
     }
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_HASH_SPLIT")) hash_split_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
@@ -387,7 +388,27 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     dah_forests(W, d_rows, d_cols, f);
     const uint32_t top = top_fuse_nodes(W, n);
     const uint32_t stop = top ? top : 1;
-    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) return rc;
+    // The leaves and wide levels of the two halves of a batch run on two
+    // streams, so one half's level launches fill the chip while the other's
+    // last partial round of workgroups drains (levels 3-8 of a k = 128 batch
+    // lose 10-60 % to that tail alone; +1.8 % squares/s,
+    // profiles/r02_hash_split.txt).  CDA_HASH_SPLIT=0 turns it off; stage
+    // profiling (bench's separate stage pass) uses the one-stream schedule so
+    // every stage's events time its own kernels.
+    if (hash_split_ > 1 && n >= 2 && !profiling_) {
+        const uint32_t h = n / 2;
+        hipEvent_t go = sync_event(0), done = sync_event(1);
+        if (!go || !done) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
+        if ((rc = check(hipEventRecord(go, s), "hipEventRecord"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(aux_stream_, go, 0), "hipStreamWaitEvent"))) return rc;
+        Forest p2[2];
+        if ((rc = dah_chunk(d_eds, k, h, n - h, stop, d_err, f, p2, aux_stream_))) return rc;
+        if ((rc = dah_chunk(d_eds, k, 0, h, stop, d_err, f, post, s))) return rc;
+        if ((rc = check(hipEventRecord(done, aux_stream_), "hipEventRecord"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent"))) return rc;
+    } else if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) {
+        return rc;
+    }
     return dah_finish(k, n, stop, post, d_roots, d_err, d_status, s);
 }
 
@@ -482,12 +503,12 @@ hipEvent_t Engine::sync_event(size_t i) {
 }
 
 // Batch pipeline.  The batch is cut into chunks of c squares; chunk i's RS
-// extension runs on rs_stream_ and its leaves and wide NMT levels on the
+// extension runs on aux_stream_ and its leaves and wide NMT levels on the
 // caller's stream after an event, so the RS of chunk i+1 (memory-bound: its
 // half-footprint kernel leaves room for hash waves on every CU) runs under the
 // SHA-256 of chunk i (VALU-bound).  The narrow levels, the tree tops and the
 // data roots -- latency-bound -- run once for the whole batch at the end.
-// rs_stream_ starts after the work already queued on `s` and `s` waits for
+// aux_stream_ starts after the work already queued on `s` and `s` waits for
 // every chunk's RS before hashing it, so the call keeps single-stream
 // semantics for the caller.  Events are re-recorded by later calls only after
 // hipStreamWaitEvent has captured them (HIP semantics).
@@ -513,13 +534,13 @@ int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uin
     if (!start || !sync_event(n_chunks)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
     if ((rc = dah_prepare(W, n, d_err, s))) return rc;
     if ((rc = check(hipEventRecord(start, s), "hipEventRecord"))) return rc;
-    if ((rc = check(hipStreamWaitEvent(rs_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(aux_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
     for (uint32_t i = 0; i < n_chunks; i++) {
         const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
-        if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, d_eds + i0 * eds_sq, rs_stream_)))
+        if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, d_eds + i0 * eds_sq, aux_stream_)))
             return rc;
         hipEvent_t ev = sync_event(1 + i);
-        if ((rc = check(hipEventRecord(ev, rs_stream_), "hipEventRecord"))) return rc;
+        if ((rc = check(hipEventRecord(ev, aux_stream_), "hipEventRecord"))) return rc;
     }
     Forest f[2], post[2];
     dah_forests(W, d_rows, d_cols, f);
