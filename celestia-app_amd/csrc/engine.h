@@ -229,8 +229,8 @@ class Engine {
     void dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]);
     int dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
                   const Forest (&f)[2], Forest (&post)[2], hipStream_t s);
-    int dah_finish(uint32_t k, uint32_t n, uint32_t from, Forest (&f)[2], uint8_t* d_roots, uint32_t* d_err,
-                   int32_t* d_status, hipStream_t s);
+    int dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const Forest (&f)[2], uint8_t* d_roots,
+                   uint32_t* d_err, int32_t* d_status, hipStream_t s);
     int enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                                   uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
                                   hipStream_t s);

@@ -332,16 +332,29 @@ int Engine::dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m,
 }
 
 // The levels below `from` nodes per tree (f = dah_chunk's post), the fused
-// tree top and the data root (which also writes d_status), for all n squares.
-int Engine::dah_finish(uint32_t k, uint32_t n, uint32_t from, Forest (&f)[2], uint8_t* d_roots, uint32_t* d_err,
-                       int32_t* d_status, hipStream_t s) {
+// tree top and the data root (which also writes d_status), for squares
+// [i0, i0 + n) of the batch (d_roots, d_err, d_status: batch base pointers).
+int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const Forest (&fb)[2], uint8_t* d_roots,
+                       uint32_t* d_err, int32_t* d_status, hipStream_t s) {
     const uint32_t W = 2 * k;
     const uint64_t slots_sq = (uint64_t)W * W * kSlot;
     int rc;
+    Forest f[2] = {fb[0], fb[1]};
+    for (int i = 0; i < 2; i++) {
+        f[i].in += i0 * f[i].in_sq;
+        if (f[i].roots) f[i].roots += i0 * f[i].roots_sq;
+        if (f[i].root_slots) f[i].root_slots += i0 * f[i].rslot_sq;
+    }
+    uint32_t* dig = dig_.as<uint32_t>() + (size_t)i0 * 2 * W * 8;
+    uint8_t* rslots = root_slots_.as<uint8_t>() + (size_t)i0 * 2 * W * kSlot;
+    if (d_roots) d_roots += (size_t)i0 * 32;
+    d_err += i0;
+    if (d_status) d_status += i0;
     // Wide per-level launches while a level has at least a wave per SIMD of
     // parents; the latency-bound rest of the trees (and the data root's RFC
     // leaf digests) in one tree_top_kernel launch.
-    uint32_t top = top_fuse_nodes(W, n);
+    // (from == 1: the chunks already produced the roots -- no tree top)
+    uint32_t top = from > 1 ? top_fuse_nodes(W, n) : 0;
     if (top > from) top = from;
     if (from > 1) {
         const uint32_t stop = top ? top : 1;
@@ -349,28 +362,24 @@ int Engine::dah_finish(uint32_t k, uint32_t n, uint32_t from, Forest (&f)[2], ui
         if (from > stop) {
             // the chunks ran ctz(W) - ctz(from) levels, the first into lvl_
             const bool in_lvl = ((__builtin_ctz(W) - __builtin_ctz(from)) & 1) != 0;
-            uint8_t* a = in_lvl ? leaf_.as<uint8_t>() : lvl_.as<uint8_t>();
-            uint8_t* b = in_lvl ? lvl_.as<uint8_t>() : leaf_.as<uint8_t>();
+            uint8_t* a = (in_lvl ? leaf_.as<uint8_t>() : lvl_.as<uint8_t>()) + i0 * slots_sq;
+            uint8_t* b = (in_lvl ? lvl_.as<uint8_t>() : leaf_.as<uint8_t>()) + i0 * slots_sq;
             const uint64_t off[2] = {0, slots_sq / 2};
             if ((rc = run_forests(f, 2, from, n, a, b, slots_sq, off, s, stop))) return rc;
         }
-        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig_.as<uint32_t>() : nullptr, 2 * W, s),
-                               "nmt tree top")))
+        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig : nullptr, 2 * W, s), "nmt tree top")))
             return rc;
         mark_end(s);
     }
     // the data-root launch also writes the per-square push-order status
     if (d_roots && top) {
         mark_begin(kStageDataRoot, s);
-        if ((rc = check(launch_data_root_digests(dig_.as<uint32_t>(), 2 * W, n, d_roots, s, d_err, d_status),
-                        "data root")))
+        if ((rc = check(launch_data_root_digests(dig, 2 * W, n, d_roots, s, d_err, d_status), "data root")))
             return rc;
         mark_end(s);
     } else if (d_roots) {   // NULL: roots only (repair verification needs no data root)
         mark_begin(kStageDataRoot, s);
-        if ((rc = check(launch_data_root_slots(root_slots_.as<uint8_t>(), 2 * W, n, dig_.as<uint32_t>(), d_roots, s,
-                                               d_err, d_status),
-                        "data root")))
+        if ((rc = check(launch_data_root_slots(rslots, 2 * W, n, dig, d_roots, s, d_err, d_status), "data root")))
             return rc;
         mark_end(s);
     }
@@ -401,15 +410,18 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
         if (!go || !done) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
         if ((rc = check(hipEventRecord(go, s), "hipEventRecord"))) return rc;
         if ((rc = check(hipStreamWaitEvent(aux_stream_, go, 0), "hipStreamWaitEvent"))) return rc;
+        // each half also finishes its own trees and data roots, so one half's
+        // latency-bound data root runs under the other half's levels
         Forest p2[2];
         if ((rc = dah_chunk(d_eds, k, h, n - h, stop, d_err, f, p2, aux_stream_))) return rc;
+        if ((rc = dah_finish(k, h, n - h, stop, p2, d_roots, d_err, d_status, aux_stream_))) return rc;
         if ((rc = dah_chunk(d_eds, k, 0, h, stop, d_err, f, post, s))) return rc;
+        if ((rc = dah_finish(k, 0, h, stop, post, d_roots, d_err, d_status, s))) return rc;
         if ((rc = check(hipEventRecord(done, aux_stream_), "hipEventRecord"))) return rc;
-        if ((rc = check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent"))) return rc;
-    } else if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) {
-        return rc;
+        return check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent");
     }
-    return dah_finish(k, n, stop, post, d_roots, d_err, d_status, s);
+    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) return rc;
+    return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -554,7 +566,7 @@ int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uin
             post[1] = p[1];
         }
     }
-    return dah_finish(k, n, stop, post, d_roots, d_err, d_status, s);
+    return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
 }
 
 int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n,

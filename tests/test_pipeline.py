@@ -69,3 +69,22 @@ def test_pipeline_push_order_status_per_square():
         pc.close()
     assert list(status != 0) == [False, False, False, True, False]
     assert np.array_equal(roots[[0, 1, 2, 4]], ref[3][[0, 1, 2, 4]])
+
+
+@pytest.mark.parametrize("k,n", [(128, 2), (128, 5), (64, 3), (16, 4), (2, 2)])
+def test_hash_split_matches_one_stream(ctx, k, n):
+    """The default schedule hashes a batch's two halves on two streams, each
+    finishing its own trees (fused tree top for small batches) and data roots;
+    CDA_HASH_SPLIT=0 is the one-stream schedule.  Same bytes, and the last
+    square's data root equals the oracle's."""
+    ods = np.stack([coracle.random_square(k, 100 + i) for i in range(n)])
+    got = da.extend_dah_batch(ods, ctx=ctx)
+    pc = _ctx_with({"CDA_HASH_SPLIT": "0"})
+    try:
+        ref = da.extend_dah_batch(ods, ctx=pc)
+    finally:
+        pc.close()
+    for a, b in zip(ref, got):
+        assert np.array_equal(a, b)
+    assert bytes(got[3][-1]) == coracle.extend_dah(ods[-1])[3]
+    assert bytes(got[3][0]) == coracle.extend_dah(ods[0])[3]
