@@ -28,7 +28,16 @@ struct RsJob {
     uint64_t src_sq, dst_sq;
     RsSeg seg[2];
     uint32_t n_seg;
+    // optional: err_init[y] = 0xFFFFFFFF for every square y of the launch
+    // (the push-order words of the hashing that follows, set by the RS launch
+    // instead of a separate fill)
+    uint32_t* err_init = nullptr;
 };
+#if defined(__HIPCC__)
+__device__ __forceinline__ void rs_err_init(const RsJob& job) {
+    if (job.err_init && blockIdx.x == 0 && threadIdx.x == 0) job.err_init[blockIdx.y] = 0xFFFFFFFFu;
+}
+#endif
 
 // GF(2^16) tables uploaded once per context.
 struct Gf16Dev {

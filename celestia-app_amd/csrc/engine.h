@@ -90,10 +90,13 @@ class Engine {
     int enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                            uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s);
     // RS extension only (ExtendShares).
-    int enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s);
+    // err_init (optional): n push-order words set to ~0 by the first RS launch.
+    int enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s,
+                       uint32_t* err_init = nullptr);
     // Roots + data root of existing EDSs.
+    // err_ready: d_err already holds ~0 words (enqueue_extend's err_init).
     int enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots,
-                    uint32_t* d_err, int32_t* d_status, hipStream_t s);
+                    uint32_t* d_err, int32_t* d_status, hipStream_t s, bool err_ready = false);
     int enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n, hipStream_t s);
 
     // Config 5: one square split across ranks (cda_split_* in include/cda.h).

@@ -231,13 +231,15 @@ int Engine::collect_stage_times(double* ms, uint32_t* counts, int n) {
     return CDA_OK;
 }
 
-int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s) {
+int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s,
+                           uint32_t* err_init) {
     if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
     int rc;
     const Gf16Dev t = gf16(k);
     mark_begin(kStageRsQ0, s);
     // d_ods == NULL: in place, the ODS is already in Q0 of d_eds
-    const RsJob q0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
+    RsJob q0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
+    q0.err_init = err_init;
     if ((rc = check(launch_rs(q0, k, n, t, s), "rs Q0"))) return rc;
     mark_end(s);
     mark_begin(kStageRsQ3, s);
@@ -273,6 +275,7 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
 // pipeline (enqueue_extend_dah) hashes each chunk as soon as its RS is done
 // (dah_chunk) and runs the latency-bound rest once for the whole batch
 // (dah_finish).
+// d_err == NULL: the push-order words are already set (enqueue_extend's err_init).
 int Engine::dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s) {
     const uint64_t slots_sq = (uint64_t)W * W * kSlot;
     int rc;
@@ -280,7 +283,7 @@ int Engine::dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s) 
     if ((rc = check(lvl_.ensure(slots_sq * n), "hipMalloc level slots"))) return rc;
     if ((rc = check(root_slots_.ensure((size_t)n * 2 * W * kSlot), "hipMalloc root slots"))) return rc;
     if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
-    return check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync");
+    return d_err ? check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync") : CDA_OK;
 }
 
 // Row trees: leaves (t, i); column trees: leaves (i, t) of the same leaf grid.
@@ -388,11 +391,11 @@ int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const
 }
 
 int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols,
-                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s) {
+                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s, bool err_ready) {
     if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
     const uint32_t W = 2 * k;
     int rc;
-    if ((rc = dah_prepare(W, n, d_err, s))) return rc;
+    if ((rc = dah_prepare(W, n, err_ready ? nullptr : d_err, s))) return rc;
     Forest f[2], post[2];
     dah_forests(W, d_rows, d_cols, f);
     const uint32_t top = top_fuse_nodes(W, n);
@@ -500,9 +503,10 @@ int Engine::enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint
 int Engine::enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds,
                                       uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err,
                                       int32_t* d_status, hipStream_t s) {
-    int rc = enqueue_extend(d_ods, k, n, d_eds, s);
+    // the first RS launch also sets the push-order words (no separate fill)
+    int rc = enqueue_extend(d_ods, k, n, d_eds, s, d_err);
     if (rc) return rc;
-    return enqueue_dah(d_eds, k, n, d_rows, d_cols, d_roots, d_err, d_status, s);
+    return enqueue_dah(d_eds, k, n, d_rows, d_cols, d_roots, d_err, d_status, s, true);
 }
 
 hipEvent_t Engine::sync_event(size_t i) {
@@ -675,10 +679,11 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     if ((rc = check(err_buf_.ensure((size_t)n * 4), "hipMalloc"))) return rc;
     hipStream_t s = stream_;
     if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
-    if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, n, h_eds_.as<uint8_t>(), s))) return rc;
+    if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, n, h_eds_.as<uint8_t>(), s, err_buf_.as<uint32_t>())))
+        return rc;
     if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, n, eds))) return rc;
     if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, n, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
-                          h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s)))
+                          h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s, true)))
         return rc;
     if ((rc = check(hipMemcpyAsync(rows, h_rows_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     if ((rc = check(hipMemcpyAsync(cols, h_cols_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;

@@ -317,6 +317,7 @@ constexpr bool kRs16Compute = CDA_RS16_PROBE != 1, kRs16Memory = CDA_RS16_PROBE 
 
 template <int K>
 __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const RsJob job) {
+    rs_err_init(job);
     extern __shared__ uint32_t X[];
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
@@ -535,6 +536,7 @@ __device__ void encode_block_column(const Gf16Dev& t, uint16_t* sym, uint32_t k,
 }
 
 __global__ __launch_bounds__(256) void rs16_lds_kernel(Gf16Dev t, const RsJob job, uint32_t k) {
+    rs_err_init(job);
     extern __shared__ __attribute__((aligned(16))) uint16_t sym[];
     const uint32_t cw = blockIdx.x >> 3;
     const uint32_t blk = blockIdx.x & 7;

@@ -137,6 +137,7 @@ __device__ __forceinline__ SegSel select_seg(const RsJob& j, uint32_t cw) {
 
 template <int K>
 __global__ __launch_bounds__(128, waves_per_simd<K>()) void rs8_job_kernel(const RsJob job) {
+    rs_err_init(job);
     const SegSel q = select_seg(job, blockIdx.x);
     // Uniform base pointers + 32-bit byte offsets (saddr addressing).
     const uint8_t* src = job.src + blockIdx.y * job.src_sq;

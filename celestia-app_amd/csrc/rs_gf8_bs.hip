@@ -50,6 +50,7 @@ constexpr uint32_t kLdsBytes = 8 * 8 * 8 * 64 * 4;   // E[u][tt][p][lane] dwords
 constexpr bool kCompute = CDA_RS8_PROBE != 1, kMemory = CDA_RS8_PROBE != 2, kExchange = CDA_RS8_PROBE != 3;
 
 __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob job) {
+    rs_err_init(job);
     if constexpr (CDA_RS8_PROBE == 4) return;
     extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -172,6 +173,7 @@ __device__ __forceinline__ uint32_t swap16(uint32_t v) {   // lane l <- lane l ^
 }
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job) {
+    rs_err_init(job);
     extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = threadIdx.x & 63;
