@@ -549,18 +549,25 @@ static size_t hash_lds(const void* fn) {
     return v > 0 ? (size_t)v : 0;
 }
 
+// CUs of the current device (all devices of a process are MI355X).
+static uint32_t device_cus() {
+    static const uint32_t cus = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            return 0u;
+        return (uint32_t)c;
+    }();
+    return cus;
+}
+
 // Workgroups of a hash launch over `nblocks` virtual blocks: all of them, or
 // CDA_HASH_WG_PER_CU x the device's CUs (persistent; tuning / batch pipeline).
 static uint32_t hash_grid(uint32_t nblocks) {
     static const uint32_t cap = [] {
         const char* e = getenv("CDA_HASH_WG_PER_CU");
         const int per = e ? atoi(e) : 0;
-        if (per <= 0) return 0u;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            return 0u;
-        return (uint32_t)(per * cus);
+        return per > 0 ? (uint32_t)per * device_cus() : 0u;
     }();
     return cap && nblocks > cap ? cap : nblocks;
 }

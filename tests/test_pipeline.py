@@ -71,7 +71,7 @@ def test_pipeline_push_order_status_per_square():
     assert np.array_equal(roots[[0, 1, 2, 4]], ref[3][[0, 1, 2, 4]])
 
 
-@pytest.mark.parametrize("k,n", [(128, 2), (128, 5), (64, 3), (16, 4), (2, 2)])
+@pytest.mark.parametrize("k,n", [(128, 2), (128, 5), (64, 3), (16, 4), (2, 2), (1, 3), (256, 2)])
 def test_hash_split_matches_one_stream(ctx, k, n):
     """The default schedule hashes a batch's two halves on two streams, each
     finishing its own trees (fused tree top for small batches) and data roots;

@@ -16,6 +16,39 @@
 
 using namespace cda;
 
+// Round with the shortest dependency chain written out: X = h + K + W + d off
+// the chain (h, d are 3 rounds old), e' = X + S1(e) + Ch(e,f,g), a' = e' +
+// S0(a) + (Maj(a,b,c) - d).  Measured: no faster than sha_compress for a lone
+// wave (the compiler already reassociates those adds) -- the lone wave is
+// bound by its own issue rate, ~4.25 cycles per instruction.
+__device__ __forceinline__ void sha_compress_lat(ShaState& s, uint32_t w[16]) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+    uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            wi = add3(w[i & 15], s0, w[(i - 7) & 15]) + s1;
+            w[i & 15] = wi;
+        }
+        const uint32_t X = add3(h, wi, d) + K[i];
+        const uint32_t en = add3(X, xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)), ch(e, f, g));
+        const uint32_t Z = maj(a, b, c) - d;
+        const uint32_t an = add3(en, xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)), Z);
+        h = g; g = f; f = e; e = en;
+        d = c; c = b; b = a; a = an;
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+
 __global__ __launch_bounds__(64) void lone(uint32_t* out, uint64_t* clk, int chain) {
     uint32_t w[16];
 #pragma unroll
@@ -25,6 +58,27 @@ __global__ __launch_bounds__(64) void lone(uint32_t* out, uint64_t* clk, int cha
     for (int c = 0; c < chain; c++) {
         sha_init(s);
         sha_compress(s, w);
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = s.h[i & 7] ^ (uint32_t)i;
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime();
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) x ^= w[i];
+    out[blockIdx.x * 64 + threadIdx.x] = x;
+    if (threadIdx.x == 0 && blockIdx.x == 0) clk[0] = t1 - t0;
+}
+
+// lone, with the short-dependency round (sha_compress_lat above)
+__global__ __launch_bounds__(64) void lone_lat(uint32_t* out, uint64_t* clk, int chain) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = threadIdx.x * 16 + i + blockIdx.x;
+    ShaState s;
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int c = 0; c < chain; c++) {
+        sha_init(s);
+        sha_compress_lat(s, w);
 #pragma unroll
         for (int i = 0; i < 16; i++) w[i] = s.h[i & 7] ^ (uint32_t)i;
     }
@@ -125,6 +179,10 @@ int main() {
         (void)hipDeviceSynchronize();
         (void)hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost);
         if (rep) printf("lone  wave : %.0f cycles per compression (s_memtime)\n", (double)h / chain);
+        hipLaunchKernelGGL(lone_lat, dim3(256), dim3(64), 0, 0, d, c, chain);
+        (void)hipDeviceSynchronize();
+        (void)hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost);
+        if (rep) printf("lone  wave, short-dependency round: %.0f cycles per compression (s_memtime)\n", (double)h / chain);
         hipLaunchKernelGGL(split, dim3(256), dim3(128), 0, 0, d, c, chain);
         (void)hipDeviceSynchronize();
         (void)hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost);
