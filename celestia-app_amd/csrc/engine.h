@@ -226,7 +226,10 @@ class Engine {
     hipStream_t aux_stream_ = nullptr;
     std::vector<hipEvent_t> sync_events_;
     uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
-    uint32_t hash_split_ = 2;       // CDA_HASH_SPLIT: hash the batch as two halves on two streams (0/1 = off)
+    uint32_t hash_split_ = 2;       // CDA_HASH_SPLIT: hash the batch in this many parts on as many streams (0/1 = off)
+    static constexpr uint32_t kMaxHashParts = 4;
+    hipStream_t split_streams_[kMaxHashParts - 2] = {};
+    int split_stream(uint32_t i, hipStream_t* out);
     hipEvent_t sync_event(size_t i);
     int dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s);
     void dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]);

@@ -9,6 +9,7 @@
 //   5. RFC-6962 data root                           (DataAvailabilityHeader.Hash)
 #include "engine.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -71,6 +72,8 @@ Engine::~Engine() {
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
+    for (hipStream_t q : split_streams_)
+        if (q) (void)hipStreamDestroy(q);
 }
 
 int Engine::check(hipError_t e, const char* what) {
@@ -400,28 +403,37 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     dah_forests(W, d_rows, d_cols, f);
     const uint32_t top = top_fuse_nodes(W, n);
     const uint32_t stop = top ? top : 1;
-    // The leaves and wide levels of the two halves of a batch run on two
-    // streams, so one half's level launches fill the chip while the other's
-    // last partial round of workgroups drains (levels 3-8 of a k = 128 batch
-    // lose 10-60 % to that tail alone; +1.8 % squares/s,
+    // The leaves and wide levels of the parts of a batch (CDA_HASH_SPLIT of
+    // them, default 2) run on their own streams, so one part's level launches
+    // fill the chip while another's last partial round of workgroups drains
+    // (levels 3-8 of a k = 128 batch lose 10-60 % to that tail alone;
     // profiles/r02_hash_split.txt).  CDA_HASH_SPLIT=0 turns it off; stage
     // profiling (bench's separate stage pass) uses the one-stream schedule so
     // every stage's events time its own kernels.
-    if (hash_split_ > 1 && n >= 2 && !profiling_) {
-        const uint32_t h = n / 2;
-        hipEvent_t go = sync_event(0), done = sync_event(1);
-        if (!go || !done) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
+    const uint32_t parts = std::min<uint32_t>(std::min<uint32_t>(hash_split_, n), kMaxHashParts);
+    if (parts > 1 && !profiling_) {
+        hipEvent_t go = sync_event(0);
+        if (!go || !sync_event(parts)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
         if ((rc = check(hipEventRecord(go, s), "hipEventRecord"))) return rc;
-        if ((rc = check(hipStreamWaitEvent(aux_stream_, go, 0), "hipStreamWaitEvent"))) return rc;
-        // each half also finishes its own trees and data roots, so one half's
-        // latency-bound data root runs under the other half's levels
-        Forest p2[2];
-        if ((rc = dah_chunk(d_eds, k, h, n - h, stop, d_err, f, p2, aux_stream_))) return rc;
-        if ((rc = dah_finish(k, h, n - h, stop, p2, d_roots, d_err, d_status, aux_stream_))) return rc;
-        if ((rc = dah_chunk(d_eds, k, 0, h, stop, d_err, f, post, s))) return rc;
-        if ((rc = dah_finish(k, 0, h, stop, post, d_roots, d_err, d_status, s))) return rc;
-        if ((rc = check(hipEventRecord(done, aux_stream_), "hipEventRecord"))) return rc;
-        return check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent");
+        // part p: squares [p n / parts, (p + 1) n / parts); part 0 on the
+        // caller's stream.  Each part also finishes its own trees and data
+        // roots, so one part's latency-bound data root runs under another's
+        // levels.
+        for (uint32_t p = parts; p-- > 0;) {
+            const uint32_t i0 = p * n / parts, i1 = (p + 1) * n / parts;
+            hipStream_t q = s;
+            if (p) {
+                if ((rc = split_stream(p - 1, &q))) return rc;
+                if ((rc = check(hipStreamWaitEvent(q, go, 0), "hipStreamWaitEvent"))) return rc;
+            }
+            Forest pp[2];
+            if ((rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q))) return rc;
+            if ((rc = dah_finish(k, i0, i1 - i0, stop, pp, d_roots, d_err, d_status, q))) return rc;
+            if (p && (rc = check(hipEventRecord(sync_event(p), q), "hipEventRecord"))) return rc;
+        }
+        for (uint32_t p = 1; p < parts; p++)
+            if ((rc = check(hipStreamWaitEvent(s, sync_event(p), 0), "hipStreamWaitEvent"))) return rc;
+        return CDA_OK;
     }
     if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) return rc;
     return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
@@ -507,6 +519,22 @@ int Engine::enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t
     int rc = enqueue_extend(d_ods, k, n, d_eds, s, d_err);
     if (rc) return rc;
     return enqueue_dah(d_eds, k, n, d_rows, d_cols, d_roots, d_err, d_status, s, true);
+}
+
+// Stream i of the hash split: the context's second stream, then lazily
+// created ones.
+int Engine::split_stream(uint32_t i, hipStream_t* out) {
+    if (i == 0) {
+        *out = aux_stream_;
+        return CDA_OK;
+    }
+    hipStream_t& q = split_streams_[i - 1];
+    if (!q) {
+        int rc;
+        if ((rc = check(hipStreamCreateWithFlags(&q, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    }
+    *out = q;
+    return CDA_OK;
 }
 
 hipEvent_t Engine::sync_event(size_t i) {
