@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "../../include/cda.h"
@@ -108,6 +109,9 @@ int Engine::init() {
     }
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_HASH_SPLIT")) hash_split_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_HOST_CHUNK")) host_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
+    if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
@@ -667,11 +671,59 @@ int Engine::push_order_error(const uint32_t* err_words, uint32_t n, const uint8_
 // the GPU works (24 instead of 32 MiB over the link per k = 128 square), and
 // the parity copies start as soon as the RS launches finish, on copy_out_,
 // overlapping the NMT hashing on stream_.
+// Page-locks a caller's host buffer for the duration of a call (RAII), so
+// its copies are plain DMA: both PCIe directions then run at once (a pageable
+// copy goes through the runtime's staging and serialises with the other
+// direction).  A buffer that cannot be registered -- e.g. one the caller
+// registered itself -- is used as it is.  Measured: a 16-square k = 128 batch
+// with its EDS returned 1 200 -> 1 880 squares/s, one square 1.25 -> 0.79 ms
+// (profiles/r02_host_buffers.txt).  CDA_HOST_REGISTER=0 turns it off.
+// The streams that may still copy from / to the buffer are drained before it
+// is unregistered (already idle on the normal path, which synchronises).
+struct HostPin {
+    void* p = nullptr;
+    hipStream_t s0, s1;
+    HostPin(bool on, const void* q, size_t bytes, hipStream_t a, hipStream_t b) : s0(a), s1(b) {
+        if (!on || !q || !bytes) return;
+        if (hipHostRegister(const_cast<void*>(q), bytes, hipHostRegisterDefault) == hipSuccess)
+            p = const_cast<void*>(q);
+        else
+            (void)hipGetLastError();
+    }
+    ~HostPin() {
+        if (!p) return;
+        (void)hipStreamSynchronize(s0);
+        (void)hipStreamSynchronize(s1);
+        (void)hipHostUnregister(p);
+    }
+    HostPin(const HostPin&) = delete;
+    HostPin& operator=(const HostPin&) = delete;
+};
+
+// Host copy of the ODS rows into Q0 of the caller's EDS, on a few host
+// threads (one core copies ~10 GB/s: a 16-square k = 128 batch's 128 MiB
+// would outlast the PCIe copies it runs beside).  CDA_HOST_THREADS caps them.
 void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
     const size_t row = (size_t)k * kShare, W = 2 * (size_t)k;
-    for (uint32_t sq = 0; sq < n; sq++)
-        for (uint32_t r = 0; r < k; r++)
-            memcpy(eds + ((size_t)sq * W * W + r * W) * kShare, ods + ((size_t)sq * k + r) * row, row);
+    const size_t rows = (size_t)n * k;
+    static const unsigned cap = [] {
+        const char* e = getenv("CDA_HOST_THREADS");
+        const unsigned hw = std::thread::hardware_concurrency();
+        unsigned v = e ? (unsigned)atoi(e) : 8u;
+        if (hw && v > hw) v = hw;
+        return v ? v : 1u;
+    }();
+    const unsigned nt = (unsigned)std::min<size_t>(cap, std::max<size_t>(1, rows * row / (2u << 20)));
+    auto part = [&](unsigned t) {
+        for (size_t i = rows * t / nt; i < rows * (t + 1) / nt; i++) {
+            const size_t sq = i / k, r = i % k;
+            memcpy(eds + (sq * W * W + r * W) * kShare, ods + i * row, row);
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
 }
 
 int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds) {
@@ -679,6 +731,10 @@ int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uin
     int rc;
     if ((rc = check(hipEventRecord(ev_rs_, stream_), "hipEventRecord"))) return rc;
     if ((rc = check(hipStreamWaitEvent(copy_out_, ev_rs_, 0), "hipStreamWaitEvent"))) return rc;
+    if (host_full_d2h_) {   // the whole EDS back as one contiguous copy (Q0 included)
+        if ((rc = check(hipMemcpyAsync(eds, d_eds, n * sq_b, hipMemcpyDeviceToHost, copy_out_), "D2H EDS"))) return rc;
+        return check(hipEventRecord(ev_out_, copy_out_), "hipEventRecord");
+    }
     for (uint32_t sq = 0; sq < n; sq++) {
         // Q1: rows 0..k-1, columns k..2k-1 (strided); Q2|Q3: the bottom half
         if ((rc = check(hipMemcpy2DAsync(eds + sq * sq_b + k * kShare, W * kShare, d_eds + sq * sq_b + k * kShare,
@@ -706,10 +762,25 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     if ((rc = check(h_roots_.ensure((size_t)n * 32), "hipMalloc"))) return rc;
     if ((rc = check(err_buf_.ensure((size_t)n * 4), "hipMalloc"))) return rc;
     hipStream_t s = stream_;
-    if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
-    if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, n, h_eds_.as<uint8_t>(), s, err_buf_.as<uint32_t>())))
-        return rc;
-    if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, n, eds))) return rc;
+    HostPin pin_ods(host_register_, ods, ods_b, stream_, copy_out_),
+        pin_eds(host_register_, eds, eds_b, stream_, copy_out_);
+    // With the EDS going back, the batch moves in chunks: chunk i+1's ODS goes
+    // up while chunk i's parity comes down (PCIe is full duplex); without
+    // chunks every H2D would precede every D2H.  CDA_HOST_CHUNK (squares,
+    // 0 = whole batch).
+    const size_t ods_sq = (size_t)k * k * kShare, eds_sq = (size_t)W * W * kShare;
+    const uint32_t c = eds && host_chunk_ && n > host_chunk_ ? host_chunk_ : n;
+    for (uint32_t i0 = 0; i0 < n; i0 += c) {
+        const uint32_t m = std::min(c, n - i0);
+        if ((rc = check(hipMemcpyAsync(h_ods_.as<uint8_t>() + i0 * ods_sq, ods + i0 * ods_sq, m * ods_sq,
+                                       hipMemcpyHostToDevice, s),
+                        "H2D")))
+            return rc;
+        if ((rc = enqueue_extend(h_ods_.as<uint8_t>() + i0 * ods_sq, k, m, h_eds_.as<uint8_t>() + i0 * eds_sq, s,
+                                 err_buf_.as<uint32_t>() + i0)))
+            return rc;
+        if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>() + i0 * eds_sq, k, m, eds + i0 * eds_sq))) return rc;
+    }
     if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, n, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
                           h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s, true)))
         return rc;
@@ -719,7 +790,7 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     std::vector<uint32_t> err(n);
     if ((rc = check(hipMemcpyAsync(err.data(), err_buf_.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H")))
         return rc;
-    if (eds) copy_q0(ods, k, n, eds);   // host work while the GPU runs
+    if (eds && !host_full_d2h_) copy_q0(ods, k, n, eds);   // host work while the GPU runs
     if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
     if (eds && (rc = check(hipEventSynchronize(ev_out_), "hipEventSynchronize"))) return rc;
     if (status)
@@ -734,6 +805,8 @@ int Engine::host_extend(const uint8_t* ods, uint32_t k, uint8_t* eds) {
     if ((rc = check(h_ods_.ensure(ods_b), "hipMalloc"))) return rc;
     if ((rc = check(h_eds_.ensure(eds_b), "hipMalloc"))) return rc;
     hipStream_t s = stream_;
+    HostPin pin_ods(host_register_, ods, ods_b, stream_, copy_out_),
+        pin_eds(host_register_, eds, eds_b, stream_, copy_out_);
     if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
     if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, 1, h_eds_.as<uint8_t>(), s))) return rc;
     if ((rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, 1, eds))) return rc;
@@ -751,6 +824,7 @@ int Engine::host_dah(const uint8_t* eds, uint32_t k, uint8_t* rows, uint8_t* col
     if ((rc = check(h_roots_.ensure(32), "hipMalloc"))) return rc;
     if ((rc = check(err_buf_.ensure(4), "hipMalloc"))) return rc;
     hipStream_t s = stream_;
+    HostPin pin_eds(host_register_, eds, eds_b, stream_, copy_out_);
     if ((rc = check(hipMemcpyAsync(h_eds_.ptr, eds, eds_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
     if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, 1, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
                           h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s)))
