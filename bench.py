@@ -167,16 +167,34 @@ def host_buffer_rates(ctx, k: int, n: int = 16, reps: int = 5) -> dict:
     one_roots = med(lambda: run(False, 1))
     txs = blobfactory.full_block(1, 128)
     pp = med(lambda: gsq.construct_extend_dah(txs, 128, ctx=ctx))
+    # the C-ABI call alone, with the txs already in one flat buffer (what a cgo
+    # caller passes) and output buffers reused
+    buf, off = gsq._flatten(txs)
+    wm = 2 * 128
+    prow = np.empty(wm * 90, dtype=np.uint8)
+    pcol = np.empty(wm * 90, dtype=np.uint8)
+    proot = np.empty(32, dtype=np.uint8)
+    kk, nk = C.c_uint32(), C.c_uint32()
+    kept = (C.c_uint32 * len(txs))()
+
+    def pp_call():
+        ctx.check(ctx.lib.cda_construct_extend_dah(ctx.h, ptr(buf), gsq._u64p(off), len(txs), 128, 64,
+                                                   gsq._lib.CDA_SQUARE_CONSTRUCT, None, 0, ptr(prow), ptr(pcol),
+                                                   prow.size, ptr(proot), C.byref(kk), kept, C.byref(nk)))
+
+    pp_c = med(pp_call)
     return {"k": k, "squares": n,
             "eds_to_host_squares_per_s": n / full,
             "pcie_gb_per_s": n * (k * k + 3 * k * k) * SHARE / full / 1e9,
             "roots_only_squares_per_s": n / only_roots,
             "one_square_eds_to_host_ms": 1e3 * one, "one_square_roots_only_ms": 1e3 * one_roots,
-            "process_proposal_ms": 1e3 * pp,
+            "process_proposal_ms": 1e3 * pp, "process_proposal_c_abi_ms": 1e3 * pp_c,
             "note": "cda_extend_dah_batch with reused host buffers: H2D ODS, D2H of the three parity quadrants "
                     "(the host copies Q0 from the ODS) overlapping the hashing, D2H roots; pcie_gb_per_s counts "
                     "ODS in + parity out; process_proposal_ms = cda_construct_extend_dah on a full k=128 block of "
-                    "blob txs (host txs -> data root, roots back to the host)"}
+                    "blob txs (host txs -> data root, roots back to the host) through the Python wrapper (which "
+                    "also flattens the txs and builds the root lists); process_proposal_c_abi_ms = the C call alone "
+                    "on an already flat tx buffer"}
 
 
 def cpu_model() -> str:
