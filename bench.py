@@ -249,11 +249,12 @@ def load_pmc(stage: str, field: str = "hbm_bytes_per_launch"):
     """A per-launch figure of `stage` from the committed rocprofv3 PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from separate --pmc
     passes of this bench: FETCH_SIZE / WRITE_SIZE -> HBM bytes, SQ_INSTS_VALU
-    ...), else None.  The newest summary is used unless CDA_PMC_SUMMARY names
-    one."""
+    ...), else None.  The newest summary (by round tag) is used unless
+    CDA_PMC_SUMMARY names one."""
     import glob
-    files = [PMC_SUMMARY] if PMC_SUMMARY else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
-                                                     key=os.path.getmtime)
+    # newest by round tag (r01_ < r01b_ < ... < r02_ < r02b_ < r02c_ sort by
+    # name; file times depend on how the tree was copied)
+    files = [PMC_SUMMARY] if PMC_SUMMARY else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
         return None
     try:
