@@ -88,3 +88,22 @@ def test_hash_split_matches_one_stream(ctx, k, n):
         assert np.array_equal(a, b)
     assert bytes(got[3][-1]) == coracle.extend_dah(ods[-1])[3]
     assert bytes(got[3][0]) == coracle.extend_dah(ods[0])[3]
+
+
+@pytest.mark.parametrize("bad", [0, 3])
+def test_hash_split_push_order_status(ctx, bad):
+    """Default schedule (two-part hash split; the first RS launch sets the
+    push-order words): a namespace-order violation in square `bad` -- in the
+    part on the caller's stream (0) or on the second stream (3) -- sets that
+    square's status only; the other data roots equal the oracle's."""
+    k, n = 32, 4
+    ods = np.stack([coracle.random_square(k, 200 + i) for i in range(n)])
+    sq = ods[bad].reshape(k, k, 512)
+    sq[3, 7, :29], sq[3, 8, :29] = sq[3, 8, :29].copy(), sq[3, 7, :29].copy()
+    if bytes(sq[3, 7, :29]) == bytes(sq[3, 8, :29]):
+        pytest.skip("equal namespaces")
+    _, _, _, roots, status = da.extend_dah_batch(ods, ctx=ctx)
+    assert [bool(x) for x in status != 0] == [i == bad for i in range(n)]
+    for i in range(n):
+        if i != bad:
+            assert bytes(roots[i]) == coracle.extend_dah(ods[i])[3]
