@@ -16,6 +16,9 @@
 //   pass B : wave w holds the shards of R = S/16 residues r (r + S*t,
 //            t = 0..15) and runs IFFT d = S..k/2 then FFT d = k/2..S;
 //   pass A': FFT layers d < S, write parity.
+// Passes A / A' run their groups depth-first (CDA_RS16_DFS, see grp_at): A
+// consumes the shards as their loads return, A' stores each parity pair right
+// after its last butterfly.
 // The whole codeword stays in the workgroup's registers; the two layout
 // changes are register all-to-alls between the 16 waves through 128 KiB of
 // LDS (R rounds each way), so HBM sees only the data read, the optional Q0
@@ -136,16 +139,50 @@ __device__ __forceinline__ void sfor(F&& f) {
 // butterflies.  Scalar loads return out of order, so waiting for one means
 // waiting for all: issuing the next load only after the wait keeps it in
 // flight across a whole group.
-template <int N, bool INV>
+//
+// Group order.  Breadth-first (layer by layer) or depth-first: the IFFT
+// (d rising) in post-order -- both halves of a block before the block's own
+// layer -- and the FFT (d falling) in pre-order.  Depth-first, pass A's
+// butterflies consume the shards in the order their loads return (the first
+// groups need registers 0-1 only, instead of layer 2 needing all 2S), and pass
+// A' finishes registers in order, so each pair's parity store issues right
+// after its last butterfly.
+template <int N, bool INV, bool DFS = false>
 constexpr int grp_at(int I, bool want_d) {
-    for (int l = 0; l < 16; l++) {
-        const int d = INV ? (1 << l) : ((N / 2) >> l);
-        if (d < 1 || d >= N) break;
-        const int ng = N / (2 * d);
-        if (I < ng) return want_d ? d : 2 * d * I;
-        I -= ng;
+    if constexpr (!DFS) {
+        for (int l = 0; l < 16; l++) {
+            const int d = INV ? (1 << l) : ((N / 2) >> l);
+            if (d < 1 || d >= N) break;
+            const int ng = N / (2 * d);
+            if (I < ng) return want_d ? d : 2 * d * I;
+            I -= ng;
+        }
+        return -1;
+    } else {
+        struct Frame {
+            int b, n, st;
+        };
+        Frame stk[20] = {};
+        int sp = 0, cnt = 0;
+        stk[sp++] = Frame{0, N, 0};
+        while (sp) {
+            Frame& f = stk[sp - 1];
+            if (f.n < 2) {
+                sp--;
+            } else if (f.st == 0) {
+                f.st = 1;
+                if (!INV && cnt++ == I) return want_d ? f.n / 2 : f.b;
+                stk[sp++] = Frame{f.b, f.n / 2, 0};
+            } else if (f.st == 1) {
+                f.st = 2;
+                stk[sp++] = Frame{f.b + f.n / 2, f.n / 2, 0};
+            } else {
+                if (INV && cnt++ == I) return want_d ? f.n / 2 : f.b;
+                sp--;
+            }
+        }
+        return -1;
     }
-    return -1;
 }
 
 template <int B, int E, int N>
@@ -188,42 +225,56 @@ __device__ __forceinline__ TabB load_tab_b(const uint32_t* TB, uint32_t idx) {
 // S*dt - 1: ZERO_G0 drops those multiplies at compile time (480 of the 4 608
 // butterfly multiplies of a k = 512 codeword); their tables are all zero, so
 // the result is bit-identical either way.
-template <int N, bool INV, bool ZERO_G0>
+template <int N, bool INV, bool ZERO_G0, bool DFS = false>
 constexpr bool grp_mul(int I) {
-    return I < N - 1 && !(ZERO_G0 && grp_at<N, INV>(I, false) == 0);
+    return I < N - 1 && !(ZERO_G0 && grp_at<N, INV, DFS>(I, false) == 0);
 }
-template <int N, bool INV, bool ZERO_G0>
+template <int N, bool INV, bool ZERO_G0, bool DFS = false>
 constexpr int next_mul(int I) {
     int J = I + 1;
-    while (J < N - 1 && !grp_mul<N, INV, ZERO_G0>(J)) J++;
+    while (J < N - 1 && !grp_mul<N, INV, ZERO_G0, DFS>(J)) J++;
     return J;
 }
 
+struct NoFin {   // layers_regs hook: register i holds its final value
+    template <class I>
+    __device__ __forceinline__ void operator()(I) const {}
+};
+
 // M independent register sets of N shards (pass B's residues) share every
 // butterfly constant: one table load and one VGPR copy per group serve all M.
-template <int N, bool INV, bool ZERO_G0 = false, int M = 1, class IdxF>
+template <int N, bool INV, bool ZERO_G0 = false, int M = 1, bool DFS = false, class IdxF, class Fin = NoFin>
 __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const Tab16& T,
-                                            const uint32_t* TB, IdxF idxf) {
+                                            const uint32_t* TB, IdxF idxf, Fin fin = Fin{}) {
     static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
     // The scalar loads are issued from inline asm: the compiler treats loads
     // of the (invariant) tables as freely movable and would sink a plain load
     // back next to its first use.  The wait is explicit for the same reason.
-    auto tab_ptr = [&](int I) {
-        return T.t + (size_t)idxf(grp_at<N, INV>(I, false), grp_at<N, INV>(I, true)) * kGf16TabWords;
+    // group positions are constant-evaluated here (the depth-first search does
+    // not fold as a runtime call), so the table addresses stay scalar
+    auto tab_ptr = [&](auto II) {
+        constexpr int g = grp_at<N, INV, DFS>(decltype(II)::value, false);
+        constexpr int d = grp_at<N, INV, DFS>(decltype(II)::value, true);
+        return T.t + (size_t)idxf(g, d) * kGf16TabWords;
     };
-    constexpr int F0 = next_mul<N, INV, ZERO_G0>(-1);
-    auto tab_idx = [&](int I) { return idxf(grp_at<N, INV>(I, false), grp_at<N, INV>(I, true)); };
+    auto tab_idx = [&](auto II) {
+        constexpr int g = grp_at<N, INV, DFS>(decltype(II)::value, false);
+        constexpr int d = grp_at<N, INV, DFS>(decltype(II)::value, true);
+        return idxf(g, d);
+    };
+    constexpr int F0 = next_mul<N, INV, ZERO_G0, DFS>(-1);
+    using F0c = std::integral_constant<int, (F0 < NG ? F0 : 0)>;
     TabRegs tc{};
-    if constexpr (F0 < NG) tc = load_tabs(tab_ptr(F0));
+    if constexpr (F0 < NG) tc = load_tabs(tab_ptr(F0c{}));
 #ifndef CDA_RS16_CHUNK2
     TabB bc{};
-    if constexpr (F0 < NG) bc = load_tab_b(TB, tab_idx(F0));
+    if constexpr (F0 < NG) bc = load_tab_b(TB, tab_idx(F0c{}));
 #endif
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
-        constexpr int g = grp_at<N, INV>(I, false), d = grp_at<N, INV>(I, true);
-        if constexpr (!grp_mul<N, INV, ZERO_G0>(I)) {
+        constexpr int g = grp_at<N, INV, DFS>(I, false), d = grp_at<N, INV, DFS>(I, true);
+        if constexpr (!grp_mul<N, INV, ZERO_G0, DFS>(I)) {
             sfor<0, M, 1>([&](auto mm) {
                 sfor<g, g + d, 1>([&](auto ii) {      // multiply by zero: XOR only
                     constexpr int i = N * decltype(mm)::value + decltype(ii)::value;
@@ -231,14 +282,19 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
                     hi[i + d] ^= hi[i];
                 });
             });
+            if constexpr (!INV && d == 1 && M == 1) {
+                fin(std::integral_constant<int, g>{});
+                fin(std::integral_constant<int, g + 1>{});
+            }
         } else {
-            constexpr int J = next_mul<N, INV, ZERO_G0>(I);
+            constexpr int J = next_mul<N, INV, ZERO_G0, DFS>(I);
+            using Jc = std::integral_constant<int, (J < NG ? J : 0)>;
             asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(tc.a)::"memory");   // this group's tables are here
             TabRegs tn;
-            if constexpr (J < NG) tn = load_tabs(tab_ptr(J));
+            if constexpr (J < NG) tn = load_tabs(tab_ptr(Jc{}));
 #ifndef CDA_RS16_CHUNK2
             TabB bn;
-            if constexpr (J < NG) bn = load_tab_b(TB, tab_idx(J));
+            if constexpr (J < NG) bn = load_tab_b(TB, tab_idx(Jc{}));
 #endif
             // the group's operands pass through volatile asm after the load, so
             // the scheduler cannot hoist the butterflies above it
@@ -276,6 +332,10 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
                     }
                 });
             });
+            if constexpr (!INV && d == 1 && M == 1) {
+                fin(std::integral_constant<int, g>{});
+                fin(std::integral_constant<int, g + 1>{});
+            }
             if constexpr (J < NG) {
                 tc = tn;
 #ifndef CDA_RS16_CHUNK2
@@ -285,15 +345,19 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
         }
     });
 }
+#ifndef CDA_RS16_DFS
+#define CDA_RS16_DFS 1
+#endif
+constexpr bool kRs16Dfs = CDA_RS16_DFS != 0;
 template <int N, class IdxF>
 __device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
                                           IdxF idxf) {
-    layers_regs<N, true>(lo, hi, T, TB, idxf);
+    layers_regs<N, true, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf);
 }
-template <int N, bool ZERO_G0 = false, class IdxF>
+template <int N, class IdxF, class Fin>
 __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
-                                         IdxF idxf) {
-    layers_regs<N, false, ZERO_G0>(lo, hi, T, TB, idxf);
+                                         IdxF idxf, Fin fin) {
+    layers_regs<N, false, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, fin);
 }
 
 constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
@@ -309,15 +373,53 @@ constexpr uint32_t cw_lds_bytes() {
 
 // Timing-diagnostic builds only (tools/rs16_phase_probe.sh, wrong output):
 // CDA_RS16_PROBE=1 drops the butterfly layers (memory + exchanges alone),
-// =2 drops the global loads and stores (compute + exchanges alone).
+// =2 drops the global loads and stores (compute + exchanges alone),
+// =3 gives every wave wave 0's pass-A / A' constants (scalar-cache hits).
 #ifndef CDA_RS16_PROBE
 #define CDA_RS16_PROBE 0
 #endif
 constexpr bool kRs16Compute = CDA_RS16_PROBE != 1, kRs16Memory = CDA_RS16_PROBE != 2;
 
+}  // namespace
+
+// Timeline builds only (tools/rs16_trace.sh): CDA_RS16_TRACE=1 has every wave
+// record the 100 MHz device clock at each phase boundary (slots 0-7) and its
+// XCC / HW_ID (9); =2 also waits for the data loads before pass A (slot 10);
+// CDA_RS16_TRACE_MASK selects slots.  Index: Q0 launch
+// (1024 codewords per square) from 0, Q2 launch (512) from kTrQ2.
+#ifndef CDA_RS16_TRACE
+#define CDA_RS16_TRACE 0
+#endif
+#ifndef CDA_RS16_TRACE_MASK
+#define CDA_RS16_TRACE_MASK 0xFFF
+#endif
+#if CDA_RS16_TRACE
+constexpr uint32_t kTrSlots = 12, kTrWgs = 12288, kTrQ2 = 8192;   // up to 8 squares
+__device__ unsigned long long g_rs16_trace[kTrWgs][kTrSlots][16];   // [workgroup][slot][wave]
+#endif
+
+namespace {
+
 template <int K>
 __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const RsJob job) {
     rs_err_init(job);
+#if CDA_RS16_TRACE
+    // one clock read + one store per wave and mark, the same address and value
+    // from every lane (no branch, so the marks do not split the schedule)
+    const uint32_t tr_i = (gridDim.x == 512 ? kTrQ2 : 0u) + blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t tr_w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto mark = [&](uint32_t slot, uint32_t = 0) {
+        if (!((CDA_RS16_TRACE_MASK >> slot) & 1)) return;
+        unsigned long long t;
+        asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        g_rs16_trace[tr_i][slot][tr_w] = t;
+    };
+    mark(0);
+    g_rs16_trace[tr_i][9][tr_w] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                  __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#else
+    auto mark = [](uint32_t, uint32_t = 0) {};
+#endif
     extern __shared__ uint32_t X[];
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
@@ -335,6 +437,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         __syncthreads();
     }
 #endif
+    mark(1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t off = 64 * (lane >> 3) + 4 * (lane & 7);    // lo dword; hi at +32
@@ -421,16 +524,22 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     if (kRs16Memory && c0 != kNoCopy) {
         sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * g.cpy_sh, lo[jj.value], hi[jj.value]); });
     }
+#if CDA_RS16_TRACE == 2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mark(10);
+#endif
     // `base` is re-laundered per table index (like lane_off) so the compiler
     // does not precompute all S-1 group addresses up front and spill them
     auto wave_base = [&]() {
-        uint32_t b = base;
+        uint32_t b = CDA_RS16_PROBE == 3 ? 0u : base;
         asm volatile("" : "+s"(b));
         return b;
     };
     if constexpr (kRs16Compute)
         ifft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); });
+    mark(2);
     xchg_a_to_b();
+    mark(3);
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
     // residue R*wave + q: shards R*wave + q + S*t in registers R*t + q
     // all R residues go through each butterfly group together (same constants)
@@ -449,6 +558,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
             layers_regs<16, false, true, R>(lr, hr, T, TB,
                                             [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
         }
+        mark(4);
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
             sfor<0, 16, 1>([&](auto tt) {
@@ -458,16 +568,24 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         });
     }
     xchg_b_to_a();
+    mark(5);
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
+    // parity shard j is stored as soon as its last butterfly is done
+    auto store_j = [&](auto jj) {
+        if constexpr (kRs16Memory) st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]);
+    };
     if constexpr (kRs16Compute)
-        fft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); });
+        fft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); }, store_j);
+    mark(6);
     if constexpr (!kRs16Memory) {   // keep every result live: a store no input can trigger
         uint32_t acc = 0;
         sfor<0, S, 1>([&](auto jj) { acc ^= (lo[jj.value] + hi[jj.value]) * (2u * jj.value + 1u); });
         if (acc == 0x9E3779B9u && threadIdx.x == 1023u) E[d0] = (uint8_t)acc;
         return;
     }
-    sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
+    if constexpr (!kRs16Compute)
+        sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
+    mark(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -576,6 +694,13 @@ hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s
 }
 
 }  // namespace
+
+#if CDA_RS16_TRACE
+extern "C" int cda_debug_rs16_trace(void* host, size_t bytes) {
+    if (bytes > sizeof(g_rs16_trace)) bytes = sizeof(g_rs16_trace);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rs16_trace), bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s);
 
