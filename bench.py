@@ -836,7 +836,8 @@ def main():
         torch.cuda.synchronize(dev)
         el5 = time.perf_counter() - a
         ctx.set_profiling(False)
-        st5 = stage_report(ctx.stage_times(), k5, 1)
+        # per step: the levels stage is marked twice per step (wide levels, tree top)
+        st5 = stage_report(ctx.stage_times(), k5, 1, False, n5)
         extras["k512"] = {"squares_per_s": n5 / el5, "ms_per_square": 1e3 * el5 / n5,
                           "ods_gb_per_s": n5 * k5 * k5 * SHARE / el5 / 1e9,
                           "data_root": g5.cpu().numpy().tobytes().hex(),

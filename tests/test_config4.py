@@ -137,3 +137,16 @@ def test_bench_rank_partition_and_max_time_gloo():
     assert el0 == el1, "every rank must report the same (max) time"
     assert el0 >= 4 * 0.1 - 1e-3, "the max over ranks is the slow rank's time"
     assert s0 == list(range(512)) and s1 == list(range(512, 1024))
+
+
+def test_stage_report_is_per_step():
+    """A stage marked several times per step (the levels: wide launches, then
+    the tree top) is reported per step when `steps` is given, and its rate
+    counts the whole stage's compressions once per step."""
+    sys.path.insert(0, ROOT)
+    import bench
+    st = {"nmt_levels": (2.0, 4), "nmt_leaves": (3.0, 2)}     # 2 steps: levels marked twice per step
+    r = bench.stage_report(st, 512, 1, False, 2)
+    assert r["nmt_levels"]["avg_ms"] == 1.0 and r["nmt_leaves"]["avg_ms"] == 1.5
+    want = bench.compressions(512)["nmt_levels"] / 1e-3
+    assert abs(r["nmt_levels"]["compressions_per_s"] - want) < 1e-6 * want
