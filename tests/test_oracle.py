@@ -214,3 +214,40 @@ def test_gf16_encoder_equals_lagrange_full_size(k):
     want = _lagrange_at(F, sym(data), xs_eval)
     got = sym(par)[xs_eval]
     assert np.array_equal(got, want)
+
+
+def _clmul_mod(a, b, bits, poly):
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        b >>= 1
+        a <<= 1
+        if a >> bits:
+            a ^= poly
+    return r
+
+
+@pytest.mark.parametrize("bits,poly,basis", [(8, 0x11D, pyref.CANTOR8), (16, 0x1002D, pyref.CANTOR16)])
+def test_cantor_basis_and_polynomial_are_self_consistent(bits, poly, basis):
+    """Intrinsic pin of the recalled Leopard field constants (klauspost
+    reedsolomon v1.12.1 leopard.go / leopard8.go): the
+    generator polynomial is primitive (x has order 2^bits - 1), and the basis
+    is a Cantor basis of that field, beta_0 = 1 and beta_i^2 + beta_i =
+    beta_(i-1).  A mis-recalled constant or polynomial fails this with
+    probability ~1 - 2^-bits per entry.  GF(2^8) is additionally pinned by
+    mainnet block 408 (test_block408_data_root); GF(2^16) has no reference
+    vector, so this and the Lagrange check are its pins."""
+    order = (1 << bits) - 1
+    x, n = 2, 1
+    while x != 1:
+        x = _clmul_mod(x, 2, bits, poly)
+        n += 1
+    assert n == order
+    assert basis[0] == 1 and len(basis) == bits
+    for i in range(1, bits):
+        b = basis[i]
+        assert _clmul_mod(b, b, bits, poly) ^ b == basis[i - 1]
+    # the basis spans the field: the log table built on it is a permutation
+    F = pyref.gf8() if bits == 8 else pyref.gf16()
+    assert sorted(F.log[:order + 1]) == list(range(order + 1))
