@@ -365,6 +365,7 @@ int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const
     // leaf digests) in one tree_top_kernel launch.
     // (from == 1: the chunks already produced the roots -- no tree top)
     uint32_t top = from > 1 ? top_fuse_nodes(W, n) : 0;
+    uint32_t n_dig = 2 * W;   // digests per square the tree top leaves for the data root
     if (top > from) top = from;
     if (from > 1) {
         const uint32_t stop = top ? top : 1;
@@ -377,14 +378,15 @@ int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const
             const uint64_t off[2] = {0, slots_sq / 2};
             if ((rc = run_forests(f, 2, from, n, a, b, slots_sq, off, s, stop))) return rc;
         }
-        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig : nullptr, 2 * W, s), "nmt tree top")))
+        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig : nullptr, 2 * W, s, &n_dig),
+                               "nmt tree top")))
             return rc;
         mark_end(s);
     }
     // the data-root launch also writes the per-square push-order status
     if (d_roots && top) {
         mark_begin(kStageDataRoot, s);
-        if ((rc = check(launch_data_root_digests(dig, 2 * W, n, d_roots, s, d_err, d_status), "data root")))
+        if ((rc = check(launch_data_root_digests(dig, n_dig, n, d_roots, s, d_err, d_status), "data root")))
             return rc;
         mark_end(s);
     } else if (d_roots) {   // NULL: roots only (repair verification needs no data root)

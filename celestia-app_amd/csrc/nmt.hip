@@ -18,6 +18,7 @@
 // once (4k^2 leaf hashes instead of the reference's 8k^2).  One thread per
 // leaf / per parent node; each NMT level of all 4k trees of every square in
 // the batch is one launch.  SHA-256 is pure 32-bit VALU work (no MFMA).
+#include <algorithm>
 #include <cstdlib>
 
 #include "cda_kernels.h"
@@ -306,27 +307,104 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
 }
 
 // ---------------------------------------------------------------------------
-// Fused top of the trees (latency-bound part: fewer parents than the chip has
-// wave slots).  One workgroup per tree runs every remaining level in LDS, no
-// launch per level: the first level reads the tree's m input slots from
-// global memory, later levels ping-pong between two LDS halves.  The root goes
-// out packed (90 B) and as a 96-B slot like level_kernel's, and its RFC-6962
-// leaf digest sha256(0x00 || root) -- the first step of the data root -- is
-// computed in the same workgroup (dig[sq][root0 + t]), so the data root
-// continues with launch_data_root_digests.
+// SHA-256 of one unit: a thread (PAIR = false) or a lane pair (PAIR = true,
+// sha_pair_compress: the latency-bound tails, where a wave per SIMD or fewer
+// is all the work there is).  Every message word is computed by both lanes.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kTopThreads = 128;   // one workgroup: tpw = 256 / n_in trees x n_in / 2 parents
+template <bool PAIR>
+struct Sha;
+template <>
+struct Sha<false> {
+    ShaState st;
+    __device__ __forceinline__ void init(bool) { sha_init(st); }
+    __device__ __forceinline__ void compress(uint32_t (&w)[16], bool) { sha_compress(st, w); }
+    __device__ __forceinline__ void digest(bool, uint32_t (&d)[8]) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) d[j] = st.h[j];
+    }
+};
+template <>
+struct Sha<true> {
+    ShaPair st;
+    __device__ __forceinline__ void init(bool A) { sha_pair_init(st, A); }
+    __device__ __forceinline__ void compress(uint32_t (&w)[16], bool A) { sha_pair_compress(st, w, A); }
+    __device__ __forceinline__ void digest(bool A, uint32_t (&d)[8]) const { sha_pair_digest(st, A, d); }
+};
 
-__global__ __launch_bounds__(kTopThreads) void tree_top_kernel(const Forest2 fs, uint32_t n_in, uint32_t tpw,
-                                                              uint32_t* __restrict__ dig, uint32_t n_items) {
+// HashNode (no mid-state branch: the tails mix data- and parity-left parents).
+template <bool PAIR>
+__device__ __forceinline__ void hash_node_u(const uint32_t (&L)[kSlotWords], const uint32_t (&R)[kSlotWords],
+                                            uint32_t (&o)[kSlotWords], bool A) {
+    Sha<PAIR> h;
+    h.init(A);
+    uint32_t w[16], D[8];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
+        h.compress(w, A);
+    }
+    h.digest(A, D);
+    inner_node_words(L, R, D, o);
+}
+// RFC-6962 leaf digest sha256(0x00 || slot[0:90]); I = big-endian slot words.
+template <bool PAIR>
+__device__ __forceinline__ void rfc_leaf_u(const uint32_t (&I)[kSlotWords], uint32_t (&D)[8], bool A) {
+    Sha<PAIR> h;
+    h.init(A);
+    uint32_t w[16];
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
+        h.compress(w, A);
+    }
+    h.digest(A, D);
+}
+// RFC-6962 inner digest sha256(0x01 || a || b) of two digests.
+template <bool PAIR>
+__device__ __forceinline__ void rfc_inner_u(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&D)[8], bool A) {
+    Sha<PAIR> h;
+    h.init(A);
+    uint32_t w[16];
+#pragma unroll
+    for (int blk = 0; blk < 2; blk++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(a, b, 16 * blk + j);
+        h.compress(w, A);
+    }
+    h.digest(A, D);
+}
+
+// ---------------------------------------------------------------------------
+// Fused top of the trees (latency-bound part: fewer parents than the chip has
+// wave slots).  One workgroup takes tpw trees and runs every remaining level
+// in LDS, no launch per level: the first level reads the trees' input slots
+// from global memory, later levels ping-pong between two LDS halves.  The
+// root goes out packed (90 B) and as a 96-B slot like level_kernel's.  If
+// dig is set, the workgroup also starts the data root: the RFC-6962 leaf
+// digests of its tpw roots (consecutive items of rowRoots || colRoots) and
+// `rfc_levels` inner levels over them, one digest per 2^rfc_levels roots to
+// dig[sq][item >> rfc_levels] -- the data root's throughput-heavy first levels
+// spread over all workgroups instead of one per square.  PAIR: a lane pair
+// per parent (kTopThreads pairs).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kTopThreads = 128;   // parents per workgroup: tpw = 256 / n_in trees x n_in / 2
+
+template <bool PAIR>
+__global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top_kernel(
+    const Forest2 fs, uint32_t n_in, uint32_t tpw, uint32_t* __restrict__ dig, uint32_t n_dig, uint32_t rfc_levels) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][kTopThreads][kSlotWords];
     const size_t sq = blockIdx.y;
     const uint32_t n_trees = fs.f[0].n_trees + fs.f[1].n_trees;
+    const uint32_t u = PAIR ? threadIdx.x >> 1 : threadIdx.x;   // unit (parent) index
+    const bool A = PAIR && (threadIdx.x & 1);
+    const bool writer = !A;                                    // one store per unit
     uint32_t o[kSlotWords];
     uint32_t cur = 0;
     for (uint32_t m = n_in; m >= 2; m /= 2) {
-        const uint32_t th = threadIdx.x, half = m / 2;
-        const uint32_t j = th / half, p = th % half;   // tree j of this workgroup, parent p
+        const uint32_t half = m / 2;
+        const uint32_t j = u / half, p = u % half;   // tree j of this workgroup, parent p
         const uint32_t g = blockIdx.x * tpw + j;
         if (j < tpw && g < n_trees) {
             uint32_t L[kSlotWords], R[kSlotWords];
@@ -345,42 +423,64 @@ __global__ __launch_bounds__(kTopThreads) void tree_top_kernel(const Forest2 fs,
                     R[i] = bswap32(buf[cur][j * m + 2 * p + 1][i]);
                 }
             }
-            hash_node<false>(L, R, o);   // a wave mixes data- and parity-left parents here
-            if (m > 2) {
+            hash_node_u<PAIR>(L, R, o, A);
+            if (m > 2 && writer) {
 #pragma unroll
-                for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][th][i] = o[i];
+                for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][u][i] = o[i];
             }
         }
         __syncthreads();
         cur ^= 1;
     }
-    // thread j < tpw holds tree j's root slot in o
-    const uint32_t g = blockIdx.x * tpw + threadIdx.x;
-    if (threadIdx.x >= tpw || g >= n_trees) return;
-    const bool f1 = g >= fs.f[0].n_trees;
-    const Forest& F = fs.f[f1 ? 1 : 0];
-    const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
-    if (F.roots) {
-        uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
+    // unit j < tpw holds tree j's root slot in o
+    const uint32_t g = blockIdx.x * tpw + u;
+    const bool has = u < tpw && g < n_trees;
+    uint32_t D[8];
+    if (has) {
+        const bool f1 = g >= fs.f[0].n_trees;
+        const Forest& F = fs.f[f1 ? 1 : 0];
+        const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
+        if (writer && F.roots) {
+            uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
 #pragma unroll
-        for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
-    }
-    if (F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
-    if (dig) {
-        uint32_t I[kSlotWords], w[16];
-#pragma unroll
-        for (int i = 0; i < kSlotWords; i++) I[i] = bswap32(o[i]);
-        ShaState st;
-        sha_init(st);
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-#pragma unroll
-            for (int jj = 0; jj < 16; jj++) w[jj] = rfc_leaf_msg(I, 16 * b + jj);
-            sha_compress(st, w);
+            for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
         }
-        uint4* d = reinterpret_cast<uint4*>(dig + (sq * n_items + F.root0 + t) * 8);
-        d[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
-        d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+        if (writer && F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
+        if (dig) {
+            uint32_t I[kSlotWords];
+#pragma unroll
+            for (int i = 0; i < kSlotWords; i++) I[i] = bswap32(o[i]);
+            rfc_leaf_u<PAIR>(I, D, A);
+        }
+    }
+    if (!dig) return;
+    // rfc_levels inner levels over this workgroup's tpw digests (the host only
+    // asks for them when every workgroup holds tpw trees): unit u < cnt holds
+    // digest u of the current level
+    uint32_t* dl = &buf[0][0][0];   // [unit][8]
+    uint32_t cnt = tpw;
+    for (uint32_t lv = 0; lv < rfc_levels; lv++) {
+        if (u < cnt && writer) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) dl[u * 8 + i] = D[i];
+        }
+        __syncthreads();
+        cnt /= 2;
+        if (u < cnt) {
+            uint32_t a[8], b[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                a[i] = dl[(2 * u) * 8 + i];
+                b[i] = dl[(2 * u + 1) * 8 + i];
+            }
+            rfc_inner_u<PAIR>(a, b, D, A);
+        }
+        __syncthreads();
+    }
+    if (has && writer && u < cnt) {
+        uint4* d = reinterpret_cast<uint4*>(dig + (sq * n_dig + ((blockIdx.x * tpw) >> rfc_levels) + u) * 8);
+        d[0] = make_uint4(D[0], D[1], D[2], D[3]);
+        d[1] = make_uint4(D[4], D[5], D[6], D[7]);
     }
 }
 
@@ -456,9 +556,33 @@ __global__ __launch_bounds__(256) void rfc_leaf_kernel(const uint8_t* __restrict
     d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
 }
 
-// Data root from the 2W leaf digests (rfc_leaf_kernel): one
-// workgroup per square, n/2 threads (<= 1024) hash the first inner level
-// straight from global memory, later levels ping-pong in LDS.
+// Data root from n leaf digests (rfc_leaf_kernel, or the group digests of
+// tree_top_kernel): one workgroup per square; the first inner level reads
+// global memory, later levels ping-pong in LDS.  A level of m <= 128 parents
+// (at most a wave per SIMD of lane pairs) runs a lane pair per parent, wider
+// levels a thread per parent.
+template <bool PAIR>
+__device__ __forceinline__ void data_root_level(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                uint32_t m) {
+    const uint32_t step = PAIR ? blockDim.x / 2 : blockDim.x;
+    const bool A = PAIR && (threadIdx.x & 1);
+    for (uint32_t i = PAIR ? threadIdx.x / 2 : threadIdx.x; i < m; i += step) {
+        uint32_t a[8], b[8], D[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[j] = in[(2 * i) * 8 + j];
+            b[j] = in[(2 * i + 1) * 8 + j];
+        }
+        rfc_inner_u<PAIR>(a, b, D, A);
+        if (!A) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) out[i * 8 + j] = D[j];
+        }
+    }
+}
+
+constexpr uint32_t kPairMaxParents = 128;   // 256 lanes: one wave per SIMD of the CU
+
 __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
                                                                uint8_t* __restrict__ data_roots,
                                                                const uint32_t* __restrict__ err,
@@ -469,23 +593,12 @@ __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* 
     uint32_t* src = hs;
     uint32_t* dst = hs + (n / 2) * 8;
     for (uint32_t m = n / 2; m >= 1; m >>= 1) {
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-            uint32_t A[8], B[8], w[16];
-            const uint32_t* a = m == n / 2 ? D + (2 * i) * 8 : src + (2 * i) * 8;
-#pragma unroll
-            for (int j = 0; j < 8; j++) { A[j] = a[j]; B[j] = a[8 + j]; }
-            ShaState st;
-            sha_init(st);
-#pragma unroll
-            for (int b = 0; b < 2; b++) {
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(A, B, 16 * b + j);
-                sha_compress(st, w);
-            }
-            uint32_t* o = m == n / 2 ? src + i * 8 : dst + i * 8;
-#pragma unroll
-            for (int j = 0; j < 8; j++) o[j] = st.h[j];
-        }
+        const uint32_t* in = m == n / 2 ? D : src;
+        uint32_t* out = m == n / 2 ? src : dst;
+        if (m <= kPairMaxParents && 2 * m <= blockDim.x)
+            data_root_level<true>(in, out, m);
+        else
+            data_root_level<false>(in, out, m);
         __syncthreads();
         if (m != n / 2) {
             uint32_t* t = src; src = dst; dst = t;
@@ -598,7 +711,7 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
 }
 
 hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint32_t* dig,
-                           uint32_t n_items, hipStream_t s) {
+                           uint32_t n_items, hipStream_t s, uint32_t* n_dig_out) {
     if (n_forest < 1 || n_forest > 2 || n_in < 2 || n_in > 2 * kTopThreads || (n_in & (n_in - 1)))
         return hipErrorInvalidValue;
     Forest2 fs{};
@@ -608,8 +721,23 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
         trees += f[i].n_trees;
     }
     const uint32_t tpw = 2 * kTopThreads / n_in;   // trees per workgroup
-    hipLaunchKernelGGL(tree_top_kernel, dim3((trees + tpw - 1) / tpw, n), dim3(kTopThreads), 0, s, fs, n_in, tpw, dig,
-                       n_items);
+    // RFC-6962 levels inside the workgroups: while every workgroup holds tpw
+    // of the n_items (a power of two) roots and at least 2 digests per square
+    // remain for data_root_digest_kernel
+    uint32_t lv = 0;
+    if (dig && trees == n_items && (n_items & (n_items - 1)) == 0 && tpw <= n_items)
+        while ((2u << lv) <= tpw && (n_items >> (lv + 1)) >= 2) lv++;
+    if (getenv("CDA_TOP_RFC") && atoi(getenv("CDA_TOP_RFC")) == 0) lv = 0;
+    const uint32_t n_dig = n_items >> lv;
+    if (n_dig_out) *n_dig_out = n_dig;
+    // lane pairs while they still fit in a wave per SIMD (1024 SIMDs)
+    const uint64_t parents = (uint64_t)n * trees * (n_in / 2);
+    const bool pair = 2 * parents <= 65536 && !(getenv("CDA_TOP_PAIR") && atoi(getenv("CDA_TOP_PAIR")) == 0);
+    const dim3 grid((trees + tpw - 1) / tpw, n);
+    if (pair)
+        hipLaunchKernelGGL(tree_top_kernel<true>, grid, dim3(2 * kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv);
+    else
+        hipLaunchKernelGGL(tree_top_kernel<false>, grid, dim3(kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv);
     return hipGetLastError();
 }
 
@@ -652,7 +780,10 @@ hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint3
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    const uint32_t threads = n_items / 2 < 1024 ? (n_items / 2 < 64 ? 64 : n_items / 2) : 1024;
+    // a thread per first-level parent (<= 1024), and room for the lane pairs
+    uint32_t threads = std::min<uint32_t>(n_items / 2, 1024);
+    threads = std::max<uint32_t>(threads, std::min<uint32_t>(n_items, 2 * kPairMaxParents));
+    threads = std::max<uint32_t>((threads + 63) / 64 * 64, 64);
     hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots,
                        status ? err : nullptr, status);
     return hipGetLastError();

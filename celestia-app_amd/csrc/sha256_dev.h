@@ -30,6 +30,7 @@ constexpr int kSlot = 96;       // device node slot (bytes)
 constexpr int kSlotWords = 24;
 
 CDA_HD uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+__host__ __device__ constexpr uint32_t crotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 // v_bitop3_b32: result bit = imm[(a << 2) | (b << 1) | c]
 CDA_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 CDA_HD uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA); }
@@ -90,6 +91,90 @@ CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
     s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
 
+// ---------------------------------------------------------------------------
+// Lane-pair compression, for the latency-bound tails (tree tops, data root).
+// A wave issues one VALU instruction per ~4 cycles however few lanes are
+// active, so a chain of dependent compressions costs its instruction count.
+// Lanes 2j (e-side: holds e f g h) and 2j+1 (a-side: a b c d) of a pair run
+// ONE instruction stream: per-lane rotate amounts make Sigma1 / Sigma0 (and
+// the schedule's sigma1 / sigma0) one alignbit triple; Ch / Maj one select;
+// the pair exchanges T1 and d with a DPP quad_perm swap:
+//   e-side:  T = Sigma1 + Ch + (h + K + W) = T1,  e' = T + d(partner)
+//   a-side:  T = Sigma0 + Maj             = T2,  a' = T + T1(partner)
+// Schedule: x = w[t-2] (e-side) / w[t-15] (a-side); u = sigma + w[t-7] +
+// w[t-16]; w[t] = u + sigma(partner).  12 ops per round and 7 per schedule
+// word: 1 104 instructions per compression instead of 1 384.  Both lanes of
+// a pair must be active and hold the same message words.
+// ---------------------------------------------------------------------------
+struct ShaPair {
+    uint32_t h[4];   // a-side lane: H0..H3; e-side lane: H4..H7
+};
+CDA_HD bool pair_aside() { return (__lane_id() & 1) != 0; }
+// the partner lane's x (quad_perm [1,0,3,2])
+CDA_HD uint32_t pair_swap(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false); }
+// e-side lane: e_val, a-side lane: a_val.  One v_cndmask on the constant
+// odd-lane mask, in asm: written as `A ? w[i] : w[j]` the compiler turns the
+// schedule's selects into a per-lane register index (compare/select chains).
+CDA_HD uint32_t pair_sel(uint32_t e_val, uint32_t a_val) {
+    if (__builtin_constant_p(e_val == a_val) && e_val == a_val) return e_val;
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(e_val), "v"(a_val), "s"(0xAAAAAAAAAAAAAAAAull));
+    return r;
+}
+
+CDA_HD void sha_pair_init(ShaPair& s, bool A) {
+    s.h[0] = A ? 0x6a09e667u : 0x510e527fu;
+    s.h[1] = A ? 0xbb67ae85u : 0x9b05688cu;
+    s.h[2] = A ? 0x3c6ef372u : 0x1f83d9abu;
+    s.h[3] = A ? 0xa54ff53au : 0x5be0cd19u;
+}
+
+CDA_HD void sha_pair_compress(ShaPair& s, uint32_t w[16], bool A) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    const uint32_t r1 = A ? 2u : 6u, r2 = A ? 13u : 11u, r3 = A ? 22u : 25u;   // Sigma0 / Sigma1
+    const uint32_t q1 = A ? 7u : 17u, q2 = A ? 18u : 19u, q3 = A ? 3u : 10u;   // sigma0 / sigma1
+    uint32_t v0 = s.h[0], v1 = s.h[1], v2 = s.h[2], v3 = s.h[3];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            const uint32_t e2 = w[(i - 2) & 15], a15 = w[(i - 15) & 15], w7 = w[(i - 7) & 15], w16 = w[i & 15];
+            // words of constant messages (padding blocks) fold as in sha_compress
+            const uint32_t s1c = crotr(e2, 17) ^ crotr(e2, 19) ^ (e2 >> 10);
+            const uint32_t s0c = crotr(a15, 7) ^ crotr(a15, 18) ^ (a15 >> 3);
+            if (__builtin_constant_p(s1c + s0c)) {
+                wi = s1c + s0c + w7 + w16;
+            } else {
+                const uint32_t x = pair_sel(e2, a15);
+                const uint32_t sg =
+                    xor3(__builtin_amdgcn_alignbit(x, x, q1), __builtin_amdgcn_alignbit(x, x, q2), x >> q3);
+                wi = add3(sg, w7, w16) + pair_swap(sg);
+            }
+            w[i & 15] = wi;
+        }
+        const uint32_t S = xor3(__builtin_amdgcn_alignbit(v0, v0, r1), __builtin_amdgcn_alignbit(v0, v0, r2),
+                                __builtin_amdgcn_alignbit(v0, v0, r3));
+        const uint32_t F = pair_sel(ch(v0, v1, v2), maj(v0, v1, v2));
+        const uint32_t Y = pair_sel(v3 + K[i] + wi, 0u);
+        const uint32_t T = add3(S, F, Y);
+        const uint32_t nv = T + pair_swap(pair_sel(T, v3));
+        v3 = v2; v2 = v1; v1 = v0; v0 = nv;
+    }
+    s.h[0] += v0; s.h[1] += v1; s.h[2] += v2; s.h[3] += v3;
+}
+
+// The whole digest (H0..H7) in both lanes of the pair.
+CDA_HD void sha_pair_digest(const ShaPair& s, bool A, uint32_t (&d)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t o = pair_swap(s.h[j]);
+        d[j] = pair_sel(o, s.h[j]);
+        d[4 + j] = pair_sel(s.h[j], o);
+    }
+}
+
 
 // ---------------------------------------------------------------------------
 // Constant message prefixes.  Two hot messages start with constant words:
@@ -104,7 +189,6 @@ CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
 struct ShaMid {
     uint32_t v[8];   // a..h after R0 rounds from the initial hash value
 };
-constexpr uint32_t crotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 template <int R0>
 constexpr ShaMid sha_mid(const uint32_t (&w)[16]) {
     constexpr uint32_t K[64] = CDA_SHA_K;
