@@ -115,6 +115,15 @@ CDA_HD uint32_t pair_swap(uint32_t x) { return (uint32_t)__builtin_amdgcn_update
 // e-side lane: e_val, a-side lane: a_val.  One v_cndmask on the constant
 // odd-lane mask, in asm: written as `A ? w[i] : w[j]` the compiler turns the
 // schedule's selects into a per-lane register index (compare/select chains).
+// u + (the partner lane's x) as one v_add_u32_dpp: u passes through an
+// empty asm so the compiler cannot fold the sum into a v_add3 (which takes no
+// DPP operand and would cost a v_mov + v_mov_dpp).  (An explicit asm DPP add
+// needs its own s_nop for the VALU-write -> DPP-read hazard and measured
+// slower, profiles/r02d_tail.)
+CDA_HD uint32_t pair_add(uint32_t u, uint32_t x) {
+    asm("" : "+v"(u));
+    return u + pair_swap(x);
+}
 CDA_HD uint32_t pair_sel(uint32_t e_val, uint32_t a_val) {
     if (__builtin_constant_p(e_val == a_val) && e_val == a_val) return e_val;
     uint32_t r;
@@ -150,7 +159,7 @@ CDA_HD void sha_pair_compress(ShaPair& s, uint32_t w[16], bool A) {
                 const uint32_t x = pair_sel(e2, a15);
                 const uint32_t sg =
                     xor3(__builtin_amdgcn_alignbit(x, x, q1), __builtin_amdgcn_alignbit(x, x, q2), x >> q3);
-                wi = add3(sg, w7, w16) + pair_swap(sg);
+                wi = pair_add(add3(sg, w7, w16), sg);
             }
             w[i & 15] = wi;
         }
@@ -159,7 +168,7 @@ CDA_HD void sha_pair_compress(ShaPair& s, uint32_t w[16], bool A) {
         const uint32_t F = pair_sel(ch(v0, v1, v2), maj(v0, v1, v2));
         const uint32_t Y = pair_sel(v3 + K[i] + wi, 0u);
         const uint32_t T = add3(S, F, Y);
-        const uint32_t nv = T + pair_swap(pair_sel(T, v3));
+        const uint32_t nv = pair_add(T, pair_sel(T, v3));
         v3 = v2; v2 = v1; v1 = v0; v0 = nv;
     }
     s.h[0] += v0; s.h[1] += v1; s.h[2] += v2; s.h[3] += v3;

@@ -48,19 +48,28 @@ print("RESULT " + json.dumps(out))
 
 
 def main():
+    global VARIANTS
+    if os.environ.get("TAIL_AB_VARIANTS"):   # JSON {name: {env}} replaces the default set
+        VARIANTS = json.loads(os.environ["TAIL_AB_VARIANTS"])
     ks = sys.argv[1:] or ["128", "512"]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for name, env in VARIANTS.items():
-        e = dict(os.environ, GRAFT_ROOT=root, **env)
-        p = subprocess.run([sys.executable, "-c", CHILD] + ks, env=e, capture_output=True, text=True, timeout=300)
-        line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
-        if p.returncode != 0 or not line:
-            print(name, "FAILED", p.returncode, p.stderr[-2000:])
-            sys.exit(1)
-        res[name] = json.loads(line[0][7:])
-        print(name, {k: round(v["ms"], 4) for k, v in res[name].items()}, flush=True)
-    roots = {json.dumps({k: v["root"] for k, v in r.items()}) for r in res.values()}
+    rounds = int(os.environ.get("TAIL_AB_ROUNDS", "3"))
+    for rnd in range(rounds):   # variants interleaved: box drift hits all of them alike
+        for name, env in VARIANTS.items():
+            e = dict(os.environ, GRAFT_ROOT=root, **env)
+            p = subprocess.run([sys.executable, "-c", CHILD] + ks, env=e, capture_output=True, text=True,
+                               timeout=300)
+            line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
+            if p.returncode != 0 or not line:
+                print(name, "FAILED", p.returncode, p.stderr[-2000:])
+                sys.exit(1)
+            res.setdefault(name, []).append(json.loads(line[0][7:]))
+            print(rnd, name, {k: round(v["ms"], 4) for k, v in res[name][-1].items()}, flush=True)
+    print("best of", rounds)
+    for name, rs in res.items():
+        print(f"  {name:20s}", {k: round(min(r[k]["ms"] for r in rs), 4) for k in rs[0]})
+    roots = {json.dumps({k: v["root"] for k, v in r.items()}) for rs in res.values() for r in rs}
     print("data roots agree across variants:", len(roots) == 1)
     if len(roots) != 1:
         sys.exit(2)
