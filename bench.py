@@ -851,11 +851,17 @@ def main():
         extras["k512"]["rs_roofline"] = {"bound": "hbm", "ms_per_square": rs5,
                                          "achieved": rs_bytes(k5) / (rs5 * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                                          "unit": "GB/s", "frac": rs_bytes(k5) / (rs5 * 1e-3) / 1e9 / PEAK_HBM_GBS}
-        v16 = load_pmc("rs_gf16", "SQ_INSTS_VALU")
+        v16 = load_pmc("rs_gf16", "SQ_INSTS_VALU")   # per launch of a one-square profile run
         if v16:
             lane = 2 * v16 * 64 / (rs5 * 1e-3) / 1e12
-            extras["k512"]["rs_roofline"]["valu"] = {"achieved": lane, "peak": PEAK_VALU_TOPS,
-                                                     "unit": "T lane-instr/s", "frac": lane / PEAK_VALU_TOPS}
+            clk = load_pmc("rs_gf16", "effective_clock_ghz") or 2.4
+            # a stream with half-rate ops (v_perm) issues one wave64
+            # instruction per ~4 cycles per SIMD: 1024 SIMDs x 64 lanes / 4 x clock
+            issue = 1024 * 64 / 4 * clk * 1e9 / 1e12
+            extras["k512"]["rs_roofline"]["valu"] = {
+                "achieved": lane, "peak": PEAK_VALU_TOPS, "unit": "T lane-instr/s", "frac": lane / PEAK_VALU_TOPS,
+                "half_rate_issue_ceiling": issue, "frac_of_issue_ceiling": lane / issue, "clock_ghz": clk,
+                "source": "SQ_INSTS_VALU x 64 per square (PMC summary, one-square run), clock GRBM_GUI_ACTIVE"}
         # the same square twice per submission: the latency-bound tail (top
         # NMT levels, 12-level data-root chain) is shared by both squares
         del e5

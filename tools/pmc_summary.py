@@ -34,7 +34,10 @@ def main(src: str, dst: str):
         s = short(row["Name"])
         out[s]["launches"] = int(row["Calls"])
         out[s]["avg_us"] = float(row["AverageNs"]) / 1e3
-    for sub in ("fetch", "write", "sq"):
+    import os
+    for sub in ("fetch", "write", "sq", "wait"):
+        if not os.path.exists(f"{src}/{sub}/run_counter_collection.csv"):
+            continue
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for row in csv.DictReader(open(f"{src}/{sub}/run_counter_collection.csv")):
             acc[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
@@ -51,11 +54,14 @@ def main(src: str, dst: str):
     for s, d in out.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["hbm_bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+        if d.get("SQ_WAVE_CYCLES"):   # share of wave cycles waiting on anything / on instruction issue
+            d["wait_any_frac"] = d.get("SQ_WAIT_ANY", 0) / d["SQ_WAVE_CYCLES"]
+            d["wait_inst_any_frac"] = d.get("SQ_WAIT_INST_ANY", 0) / d["SQ_WAVE_CYCLES"]
         if "SQ_INSTS_VALU" in d and d.get("SQ_WAVES"):
             d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps({k: {kk: v for kk, v in d.items() if kk in ("avg_us", "hbm_bytes_per_launch",
-                                                                  "valu_insts_per_wave", "effective_clock_ghz")}
+                                                                  "valu_insts_per_wave", "effective_clock_ghz", "wait_any_frac")}
                       for k, d in out.items() if k in STAGE.values()}, indent=1))
 
 
