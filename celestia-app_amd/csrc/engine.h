@@ -262,6 +262,12 @@ class Engine {
     bool host_full_d2h_ = false;    // CDA_HOST_FULL_D2H: EDS back as one contiguous copy (no host Q0 copy)
     bool host_register_ = true;     // CDA_HOST_REGISTER: page-lock the caller's buffers for the call (0 = off)
     hipStream_t split_streams_[kMaxHashParts - 2] = {};
+    // CDA_RS_CUS=N (batch pipeline): chunk i > 0's RS on a stream masked to N
+    // CUs, the chunks' hashing on the complement (no CU runs both kernels:
+    // their instruction streams slow each other down on a shared SIMD)
+    uint32_t rs_cus_ = 0;
+    hipStream_t rs_cu_stream_ = nullptr, hash_cu_stream_ = nullptr;
+    int make_cu_streams();
     int split_stream(uint32_t i, hipStream_t* out);
     hipEvent_t sync_event(size_t i);
     int dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s);

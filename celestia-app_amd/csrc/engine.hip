@@ -73,6 +73,8 @@ Engine::~Engine() {
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
+    if (rs_cu_stream_) (void)hipStreamDestroy(rs_cu_stream_);
+    if (hash_cu_stream_) (void)hipStreamDestroy(hash_cu_stream_);
     for (hipStream_t q : split_streams_)
         if (q) (void)hipStreamDestroy(q);
 }
@@ -113,6 +115,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
+    if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -562,6 +565,27 @@ hipEvent_t Engine::sync_event(size_t i) {
 // every chunk's RS before hashing it, so the call keeps single-stream
 // semantics for the caller.  Events are re-recorded by later calls only after
 // hipStreamWaitEvent has captured them (HIP semantics).
+// The RS / hash CU partition of CDA_RS_CUS: RS on CUs (33 j) mod ncu, j < N --
+// spread over the XCDs whether the mask bits run XCD-major or CU-major.
+int Engine::make_cu_streams() {
+    if (rs_cu_stream_) return CDA_OK;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_) != hipSuccess || ncu <= 0 ||
+        rs_cus_ >= (uint32_t)ncu)
+        return fail(CDA_ERR_INVALID, "CDA_RS_CUS must be below the device's CU count");
+    std::vector<uint32_t> rs((ncu + 31) / 32, 0u), hs((ncu + 31) / 32, 0u);
+    for (uint32_t j = 0; j < rs_cus_; j++) {
+        const uint32_t b = (33u * j) % (uint32_t)ncu;
+        rs[b / 32] |= 1u << (b % 32);
+    }
+    for (int b = 0; b < ncu; b++)
+        if (!(rs[b / 32] >> (b % 32) & 1)) hs[b / 32] |= 1u << (b % 32);
+    int rc;
+    if ((rc = check(hipExtStreamCreateWithCUMask(&rs_cu_stream_, (uint32_t)rs.size(), rs.data()), "cu mask stream")))
+        return rc;
+    return check(hipExtStreamCreateWithCUMask(&hash_cu_stream_, (uint32_t)hs.size(), hs.data()), "cu mask stream");
+}
+
 int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                                uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
                                hipStream_t s) {
@@ -580,29 +604,44 @@ int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uin
             break;
         }
     int rc;
+    const bool cu_split = rs_cus_ > 0 && !profiling_;
+    if (cu_split && (rc = make_cu_streams())) return rc;
+    // RS chunks: on aux_stream_, or (CU split) chunk 0 on the whole chip (s)
+    // and the rest on the RS CUs; hashing on s, or on the complement CUs
+    hipStream_t rs_q = cu_split ? rs_cu_stream_ : aux_stream_;
+    hipStream_t hq = cu_split ? hash_cu_stream_ : s;
     hipEvent_t start = sync_event(0);
-    if (!start || !sync_event(n_chunks)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
+    if (!start || !sync_event(n_chunks + 1)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
     if ((rc = dah_prepare(W, n, d_err, s))) return rc;
+    if (cu_split) {
+        if ((rc = enqueue_extend(d_ods, k, c, d_eds, s))) return rc;
+        if ((rc = check(hipEventRecord(sync_event(1), s), "hipEventRecord"))) return rc;
+    }
     if ((rc = check(hipEventRecord(start, s), "hipEventRecord"))) return rc;
-    if ((rc = check(hipStreamWaitEvent(aux_stream_, start, 0), "hipStreamWaitEvent"))) return rc;
-    for (uint32_t i = 0; i < n_chunks; i++) {
+    if ((rc = check(hipStreamWaitEvent(rs_q, start, 0), "hipStreamWaitEvent"))) return rc;
+    for (uint32_t i = cu_split ? 1 : 0; i < n_chunks; i++) {
         const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
-        if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, d_eds + i0 * eds_sq, aux_stream_)))
+        if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, d_eds + i0 * eds_sq, rs_q)))
             return rc;
         hipEvent_t ev = sync_event(1 + i);
-        if ((rc = check(hipEventRecord(ev, aux_stream_), "hipEventRecord"))) return rc;
+        if ((rc = check(hipEventRecord(ev, rs_q), "hipEventRecord"))) return rc;
     }
     Forest f[2], post[2];
     dah_forests(W, d_rows, d_cols, f);
     for (uint32_t i = 0; i < n_chunks; i++) {
         const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
-        if ((rc = check(hipStreamWaitEvent(s, sync_event(1 + i), 0), "hipStreamWaitEvent"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(hq, sync_event(1 + i), 0), "hipStreamWaitEvent"))) return rc;
         Forest p[2];
-        if ((rc = dah_chunk(d_eds, k, i0, m, stop, d_err, f, p, s))) return rc;
+        if ((rc = dah_chunk(d_eds, k, i0, m, stop, d_err, f, p, hq))) return rc;
         if (i == 0) {
             post[0] = p[0];
             post[1] = p[1];
         }
+    }
+    if (cu_split) {   // the latency-bound rest on the whole chip, in order on s
+        hipEvent_t done = sync_event(n_chunks + 1);
+        if ((rc = check(hipEventRecord(done, hq), "hipEventRecord"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(s, done, 0), "hipStreamWaitEvent"))) return rc;
     }
     return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
 }
