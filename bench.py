@@ -401,6 +401,33 @@ def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
     return out
 
 
+def config5_isolated(world: int, timeout_s: float) -> dict:
+    """Run config5() in a child of this rank (same RANK / WORLD_SIZE /
+    LOCAL_RANK, MASTER_PORT + 7 for the children's own process group) and
+    return rank 0's result; a hang is killed at timeout_s, a crash is reported.
+    Every rank waits for its own child only, so no collective of the parent
+    group depends on the children."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29517")) + 7)
+    env.setdefault("RANK", "0")
+    env.setdefault("WORLD_SIZE", str(world))
+    env.setdefault("LOCAL_RANK", "0")
+    cmd = [sys.executable, os.path.abspath(__file__), "--config5-child", "--no-cpu"]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        out, err = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return {"error": f"no result after {timeout_s} s (collective hang?)"}
+    lines = [ln for ln in out.splitlines() if ln.startswith("CONFIG5 ")]
+    if p.returncode != 0:
+        return {"error": f"config-5 child exited with {p.returncode}: {err.strip()[-400:]}"}
+    return json.loads(lines[-1][8:]) if lines else {"rank_result": "only rank 0 reports"}
+
+
 def square_construction(ctx, dev, stream, max_ss: int = 128, reps: int = 20) -> dict:
     """go-square square.Construct on a full k=128 block of
     blob txs (celestia_da.blobfactory.full_block), then the fused path txs ->
@@ -639,6 +666,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="skip k=512 and latency extras")
     ap.add_argument("--config5", action="store_true",
                     help="run the config-5 extra (one k=512 square split over the ranks) even at one rank")
+    ap.add_argument("--config5-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--layout", choices=("packed", "inplace"), default="inplace",
                     help="inplace: ODS already in Q0 of the EDS arena (cda_extend_dah_inplace_device, the layout "
                          "rsmt2d's EDS has; no Q0 copy); packed: ODS in its own k*k buffer "
@@ -656,13 +684,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1 or args.config5:
+    if world > 1 or args.config5 or args.config5_child:
         if world == 1:   # a one-rank group for --config5 outside torchrun
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29517")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
+
+    if args.config5_child:   # config5_isolated's child: one rank of config 5, JSON on stdout (rank 0)
+        res = config5(Context(local), dev, rank, world, 512)
+        if rank == 0:
+            print("CONFIG5 " + json.dumps(res), flush=True)
+        dist.destroy_process_group()
+        return
 
     k, B = args.k, args.batch
     W = 2 * k
@@ -924,26 +959,10 @@ def main():
     if (world > 1 or args.config5) and not args.no_extras:
         # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
         # all-to-all of the row-encoded blocks, column encode + hashing per
-        # rank, gather of subtree/column roots, combine on rank 0).  A
-        # collective that never returns must not cost the headline line: a
-        # watchdog prints it (rank 0) and ends every rank cleanly.
-        import threading
-
-        def on_timeout():
-            extras["config5"] = {"error": f"no result after {CONFIG5_TIMEOUT_S} s (collective hang?)"}
-            if rank == 0:
-                print(json.dumps(make_line(None)), flush=True)
-            os._exit(0)
-
-        wd = threading.Timer(CONFIG5_TIMEOUT_S, on_timeout)
-        wd.daemon = True
-        wd.start()
-        try:
-            extras["config5"] = config5(ctx, dev, rank, world, 512)
-        except Exception as e:  # report, never lose the headline line
-            extras["config5"] = {"error": f"{type(e).__name__}: {e}"}
-        finally:
-            wd.cancel()
+        # rank, gather of subtree/column roots, combine on rank 0), run by a
+        # child process per rank with its own process group: a collective that
+        # never returns or a crash there must not cost the headline line.
+        extras["config5"] = config5_isolated(world, CONFIG5_TIMEOUT_S)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
