@@ -962,6 +962,8 @@ def main():
         # rank, gather of subtree/column roots, combine on rank 0), run by a
         # child process per rank with its own process group: a collective that
         # never returns or a crash there must not cost the headline line.
+        if dist.is_initialized():
+            dist.barrier()   # rank 0 ran the extras meanwhile: start the children together
         extras["config5"] = config5_isolated(world, CONFIG5_TIMEOUT_S)
 
     cpu = None
