@@ -390,3 +390,20 @@ def test_torch_split_world1_rows_send_on_gpu(ctx, k):
     assert np.array_equal(block.cpu().numpy().reshape(-1, 512), e_eds)
     assert np.array_equal(rows.cpu().numpy(), e_rows) and np.array_equal(cols.cpu().numpy(), e_cols)
     assert root.cpu().numpy().tobytes() == e_root
+
+
+@pytest.mark.parametrize("k", [128, 512])
+def test_extension_is_linear_full_size(ctx, k):
+    """Size-independent property at the bench sizes (configs 2-4 and 3): the
+    extension is GF(2)-linear, EDS(a ^ b) == EDS(a) ^ EDS(b), and the ODS
+    comes back unchanged in Q0 (any bytes: extension never checks namespaces)."""
+    rng = np.random.default_rng(k + 11)
+    a = rng.integers(0, 256, (k * k, 512), dtype=np.uint8)
+    b = rng.integers(0, 256, (k * k, 512), dtype=np.uint8)
+    ea = da.extend_shares(a).array().reshape(2 * k, 2 * k, 512)
+    eb = da.extend_shares(b).array().reshape(2 * k, 2 * k, 512)
+    ex = da.extend_shares(a ^ b).array().reshape(2 * k, 2 * k, 512)
+    assert np.array_equal(ea[:k, :k].reshape(-1, 512), a)
+    assert np.array_equal(ex, ea ^ eb)
+    # idempotence: a second extension of the same ODS gives the same bytes
+    assert np.array_equal(da.extend_shares(a).array().reshape(2 * k, 2 * k, 512), ea)
