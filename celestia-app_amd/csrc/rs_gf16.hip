@@ -243,9 +243,14 @@ struct NoFin {   // layers_regs hook: register i holds its final value
 
 // M independent register sets of N shards (pass B's residues) share every
 // butterfly constant: one table load and one VGPR copy per group serve all M.
-template <int N, bool INV, bool ZERO_G0 = false, int M = 1, bool DFS = false, class IdxF, class Fin = NoFin>
+// lidxf (optional): index of a group's constant relative to TB, when TB
+// already includes a runtime (per-wave) base -- then the LDS reads are one
+// VGPR base + immediate offsets instead of an SGPR address copied to a VGPR
+// per group.
+template <int N, bool INV, bool ZERO_G0 = false, int M = 1, bool DFS = false, class IdxF, class Fin = NoFin,
+          class LIdxF = std::nullptr_t>
 __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const Tab16& T,
-                                            const uint32_t* TB, IdxF idxf, Fin fin = Fin{}) {
+                                            const uint32_t* TB, IdxF idxf, Fin fin = Fin{}, LIdxF lidxf = nullptr) {
     static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
     // The scalar loads are issued from inline asm: the compiler treats loads
@@ -261,7 +266,10 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
     auto tab_idx = [&](auto II) {
         constexpr int g = grp_at<N, INV, DFS>(decltype(II)::value, false);
         constexpr int d = grp_at<N, INV, DFS>(decltype(II)::value, true);
-        return idxf(g, d);
+        if constexpr (std::is_same_v<LIdxF, std::nullptr_t>)
+            return idxf(g, d);
+        else
+            return lidxf(g, d);
     };
     constexpr int F0 = next_mul<N, INV, ZERO_G0, DFS>(-1);
     using F0c = std::integral_constant<int, (F0 < NG ? F0 : 0)>;
@@ -349,15 +357,15 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
 #define CDA_RS16_DFS 1
 #endif
 constexpr bool kRs16Dfs = CDA_RS16_DFS != 0;
-template <int N, class IdxF>
+template <int N, class IdxF, class LIdxF>
 __device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
-                                          IdxF idxf) {
-    layers_regs<N, true, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf);
+                                          IdxF idxf, LIdxF lidxf) {
+    layers_regs<N, true, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, NoFin{}, lidxf);
 }
-template <int N, class IdxF, class Fin>
+template <int N, class IdxF, class Fin, class LIdxF>
 __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
-                                         IdxF idxf, Fin fin) {
-    layers_regs<N, false, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, fin);
+                                         IdxF idxf, Fin fin, LIdxF lidxf) {
+    layers_regs<N, false, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, fin, lidxf);
 }
 
 constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
@@ -424,7 +432,12 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
     const Tab16 T{tab};
-    const uint32_t* TB = X + kXchgBytes / 4;
+    // the table region's LDS address as a VGPR (not a folded constant), so
+    // every table read below is this base (+ a per-wave offset, one v_add
+    // per pass) with the constant's index in the instruction's offset field
+    uint32_t tb_addr = kXchgBytes;
+    asm volatile("" : "+v"(tb_addr));
+    const uint32_t* TB = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(X) + tb_addr);
 #ifndef CDA_RS16_CHUNK2
     {   // stage dwords 12..19 of every constant's record (its src1 halves)
         uint32_t* tb = X + kXchgBytes / 4;
@@ -451,22 +464,21 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     const uint32_t s0 = g.src_off + c * g.src_cw, ss = g.src_sh;      // data shard i
     const uint32_t d0 = g.dst_off + c * g.dst_cw, ds = g.dst_sh;      // parity / scratch shard i
     const uint32_t c0 = g.cpy_off == kNoCopy ? kNoCopy : g.cpy_off + c * g.cpy_cw;
-    // `lo_off` is re-laundered at every use site so the compiler recomputes
-    // (one v_add) instead of keeping dozens of per-shard addresses live.
-    auto lane_off = [&]() {
-        uint32_t o = off;
-        asm volatile("" : "+v"(o));
-        return o;
-    };
+    // A shard's uniform byte offset is added to the base pointer in SGPRs
+    // (SALU) at the use site -- laundered there, so the compiler neither keeps
+    // dozens of per-shard pointers live nor moves the add into VALU -- and
+    // every access is that pointer + the lane's fixed VGPR offset (saddr).
     auto ld = [&](const uint8_t* base, uint32_t o, uint32_t& l, uint32_t& h) {
-        const uint32_t a = o + lane_off();
-        l = *reinterpret_cast<const uint32_t*>(base + a);
-        h = *reinterpret_cast<const uint32_t*>(base + a + 32);
+        asm volatile("" : "+s"(o));
+        const uint8_t* p = base + o;
+        l = *reinterpret_cast<const uint32_t*>(p + off);
+        h = *reinterpret_cast<const uint32_t*>(p + off + 32);
     };
     auto st = [&](uint8_t* base, uint32_t o, uint32_t l, uint32_t h) {
-        const uint32_t a = o + lane_off();
-        *reinterpret_cast<uint32_t*>(base + a) = l;
-        *reinterpret_cast<uint32_t*>(base + a + 32) = h;
+        asm volatile("" : "+s"(o));
+        uint8_t* p = base + o;
+        *reinterpret_cast<uint32_t*>(p + off) = l;
+        *reinterpret_cast<uint32_t*>(p + off + 32) = h;
     };
 
     // The whole codeword (K shards x 512 B = 256 KiB at K = 512) stays in the
@@ -536,7 +548,8 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         return b;
     };
     if constexpr (kRs16Compute)
-        ifft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); });
+        ifft_regs<S>(lo, hi, T, TB + 8 * S * (CDA_RS16_PROBE == 3 ? 0u : wave), [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); },
+                     [](int g, int d) { return (uint32_t)(K - 1 + g + d); });
     mark(2);
     xchg_a_to_b();
     mark(3);
@@ -575,7 +588,8 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         if constexpr (kRs16Memory) st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]);
     };
     if constexpr (kRs16Compute)
-        fft_regs<S>(lo, hi, T, TB, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); }, store_j);
+        fft_regs<S>(lo, hi, T, TB + 8 * S * (CDA_RS16_PROBE == 3 ? 0u : wave), [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); },
+                    store_j, [](int g, int d) { return (uint32_t)(g + d - 1); });
     mark(6);
     if constexpr (!kRs16Memory) {   // keep every result live: a store no input can trigger
         uint32_t acc = 0;
