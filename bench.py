@@ -313,7 +313,7 @@ def cpu_baseline(k: int, seconds: float, threads: int, runs: int = 5):
                       f"visible CPUs, {cpu_model()})"}
 
 
-def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
+def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5, emit=None) -> dict:
     """Config 5 timing: one k x k square split over `world`
     GPUs, by both drivers of the same kernels: the library's own RCCL
     communicator (cda_comm_init + cda_extend_dah_split, what a cgo host uses)
@@ -369,7 +369,21 @@ def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
         return bool(torch.equal(ref[2], root) and torch.equal(ref[0], rows) and torch.equal(ref[1], cols)
                     and int(err.item()) == 0xFFFFFFFF)
 
-    # (1) library RCCL communicator
+    # (1) torch.distributed collectives (every rank enters every collective even
+    # if a local step fails)
+    ops = cdist.GpuSplitOps(ctx, dev)
+    errors = []
+    el, res = timed(lambda: cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append))
+    el, bad = max_over_ranks(el, len(errors))
+    if bad:
+        out["torch_distributed"] = {"error": repr(errors[0]) if errors else "failed on another rank"}
+    else:
+        out["torch_distributed"] = {"ms_per_square": 1e3 * el / iters, "squares_per_s": iters / el}
+        if rank == 0:
+            out["torch_distributed"]["matches_single_gpu"] = matches(res[2])
+    if emit:
+        emit(out)   # a hang in the next leg keeps this one's result
+    # (2) library RCCL communicator
     try:
         uid = torch.zeros(128, dtype=torch.uint8, device=on)
         if rank == 0:
@@ -386,18 +400,6 @@ def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5) -> dict:
         c.close()
     except Exception as ex:  # report, keep the torch.distributed leg
         out["library_rccl"] = {"error": f"{type(ex).__name__}: {ex}"}
-    # (2) torch.distributed collectives (every rank enters every collective even
-    # if a local step fails)
-    ops = cdist.GpuSplitOps(ctx, dev)
-    errors = []
-    el, res = timed(lambda: cdist.extend_dah_split(mine, k, ops, rank, world, on_error=errors.append))
-    el, bad = max_over_ranks(el, len(errors))
-    if bad:
-        out["torch_distributed"] = {"error": repr(errors[0]) if errors else "failed on another rank"}
-    else:
-        out["torch_distributed"] = {"ms_per_square": 1e3 * el / iters, "squares_per_s": iters / el}
-        if rank == 0:
-            out["torch_distributed"]["matches_single_gpu"] = matches(res[2])
     return out
 
 
@@ -411,21 +413,30 @@ def config5_isolated(world: int, timeout_s: float) -> dict:
     env = dict(os.environ)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29517")) + 7)
+    # under torch.distributed.run the env:// rendezvous would join the launch
+    # agent's store (on the parent's port); the children's rank 0 hosts its own
+    env["TORCHELASTIC_USE_AGENT_STORE"] = "False"
     env.setdefault("RANK", "0")
     env.setdefault("WORLD_SIZE", str(world))
     env.setdefault("LOCAL_RANK", "0")
     cmd = [sys.executable, os.path.abspath(__file__), "--config5-child", "--no-cpu"]
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    res = {}
     try:
         out, err = p.communicate(timeout=timeout_s)
     except subprocess.TimeoutExpired:
         p.kill()
-        p.communicate()
-        return {"error": f"no result after {timeout_s} s (collective hang?)"}
-    lines = [ln for ln in out.splitlines() if ln.startswith("CONFIG5 ")]
-    if p.returncode != 0:
-        return {"error": f"config-5 child exited with {p.returncode}: {err.strip()[-400:]}"}
-    return json.loads(lines[-1][8:]) if lines else {"rank_result": "only rank 0 reports"}
+        out, err = p.communicate()
+        res["error"] = f"no result after {timeout_s} s (collective hang?)"
+    for ln in out.splitlines():   # the legs reported so far (rank 0's child)
+        if ln.startswith("CONFIG5 "):
+            res.update(json.loads(ln[8:]))
+    if p.returncode not in (0, None) and "error" not in res and p.returncode != -9:
+        res["error"] = f"config-5 child exited with {p.returncode}"
+    if "error" in res:   # the child's last words, minus the runtime's noise
+        tail = [ln for ln in err.splitlines() if "amdgpu.ids" not in ln and "hostname of the client" not in ln]
+        res["child_stderr_tail"] = "\n".join(tail)[-600:]
+    return res or {"rank_result": "only rank 0 reports"}
 
 
 def square_construction(ctx, dev, stream, max_ss: int = 128, reps: int = 20) -> dict:
@@ -682,6 +693,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (never set by the driver): CDA_BENCH_DEVICE puts every
+    # rank on one device and CDA_BENCH_BACKEND=gloo replaces RCCL for the
+    # parent group, so the N > 1 flow runs on a one-GPU box
+    if os.environ.get("CDA_BENCH_DEVICE"):
+        local = int(os.environ["CDA_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or args.config5 or args.config5_child:
@@ -690,12 +706,14 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29517")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CDA_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     if args.config5_child:   # config5_isolated's child: one rank of config 5, JSON on stdout (rank 0)
-        res = config5(Context(local), dev, rank, world, 512)
-        if rank == 0:
-            print("CONFIG5 " + json.dumps(res), flush=True)
+        def emit(part):
+            if rank == 0:
+                print("CONFIG5 " + json.dumps(part), flush=True)
+        emit(config5(Context(local), dev, rank, world, 512, emit=emit))
         dist.destroy_process_group()
         return
 
@@ -754,7 +772,7 @@ def main():
             assert parity["matched"] == parity["checked"], f"data roots differ from the oracle fixture: {parity}"
 
     def reduce_max(x: float) -> float:
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
