@@ -407,3 +407,53 @@ def test_extension_is_linear_full_size(ctx, k):
     assert np.array_equal(ex, ea ^ eb)
     # idempotence: a second extension of the same ODS gives the same bytes
     assert np.array_equal(da.extend_shares(a).array().reshape(2 * k, 2 * k, 512), ea)
+
+
+def test_threads_and_streams_on_one_context(ctx):
+    """Six host threads, each with its own stream, enqueue device calls of
+    different shapes (single squares: lane-pair tree tops; batches: wide
+    levels) on ONE context with no host sync in between -- the cgo situation
+    of several goroutines sharing a device context.  Every data root and
+    every row/column root equals the oracle."""
+    import threading
+    import torch
+    dev = torch.device("cuda", 0)
+    shapes = [(16, 1), (32, 3), (64, 1), (128, 1), (64, 2), (8, 5)]
+    jobs = []
+    for j, (k, n) in enumerate(shapes):
+        W = 2 * k
+        ods = np.stack([coracle.random_square(k, 500 + 10 * j + i) for i in range(n)])
+        jobs.append(dict(k=k, n=n, ods=ods, o=torch.from_numpy(ods.reshape(n, -1)).to(dev),
+                         e=torch.empty(n, W * W * 512, dtype=torch.uint8, device=dev),
+                         r=torch.empty(n, W * 90, dtype=torch.uint8, device=dev),
+                         c=torch.empty(n, W * 90, dtype=torch.uint8, device=dev),
+                         g=torch.empty(n, 32, dtype=torch.uint8, device=dev),
+                         s=torch.cuda.Stream(dev)))
+    torch.cuda.synchronize()
+    errs = []
+    go = threading.Barrier(len(jobs))
+
+    def worker(jb):
+        try:
+            go.wait()
+            for _ in range(3):
+                ctx.extend_dah_device(jb["o"].data_ptr(), jb["k"], jb["n"], jb["e"].data_ptr(), jb["r"].data_ptr(),
+                                      jb["c"].data_ptr(), jb["g"].data_ptr(), None, jb["s"].cuda_stream)
+        except Exception as ex:  # reported below
+            errs.append(repr(ex))
+
+    ts = [threading.Thread(target=worker, args=(jb,)) for jb in jobs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert errs == []
+    for jb in jobs:
+        W = 2 * jb["k"]
+        for i in range(jb["n"]):
+            e_eds, e_rows, e_cols, e_root = (coracle.cpu_baseline(jb["ods"][i], 8) if jb["k"] >= 64
+                                             else coracle.extend_dah(jb["ods"][i]))
+            assert np.array_equal(jb["r"][i].cpu().numpy().reshape(W, 90), e_rows), (jb["k"], i)
+            assert np.array_equal(jb["c"][i].cpu().numpy().reshape(W, 90), e_cols), (jb["k"], i)
+            assert jb["g"][i].cpu().numpy().tobytes() == e_root, (jb["k"], i)
