@@ -106,12 +106,18 @@ def time_region(step, steps: int, sync, world: int, reduce_max=None, barrier=Non
 
 
 def golden_config4():
-    """tests/golden/config4_k128.json (oracle digests of squares 0..127,
-    oracle/gen_config4.py), or None."""
+    """tests/golden/config4_k128.json (oracle digests of squares 0..127) merged
+    with config4_k128_rest.json (data roots of squares 128..1023; both by
+    oracle/gen_config4.py), so every rank's shard is checked; or None."""
     p = os.path.join(ROOT, "tests", "golden", "config4_k128.json")
     try:
         with open(p) as f:
-            return json.load(f)
+            g = json.load(f)
+        rest = os.path.join(ROOT, "tests", "golden", "config4_k128_rest.json")
+        if os.path.exists(rest):
+            with open(rest) as f:
+                g["squares"].update(json.load(f)["squares"])
+        return g
     except OSError:
         return None
 
@@ -993,7 +999,7 @@ def main():
                                    f"(rank g: squares [{B}g, {B}g+{B}); x8 GPUs = config 4's 1024)",
                        "k": k, "squares_per_gpu_per_step": B, "distinct_squares": nd,
                        "parallelism": f"dp{world} (independent squares)", "layout": args.layout},
-            "parity": {**parity, "fixture": "tests/golden/config4_k128.json (oracle data roots)"},
+            "parity": {**parity, "fixture": "tests/golden/config4_k128{,_rest}.json (oracle data roots of squares 0..1023)"},
             "ods_gb_per_s": value * k * k * SHARE / 1e9,
             "stage_pass": {"steps": n_prof, "ms_per_step": 1e3 * el_prof / n_prof,
                            "note": "stages and rooflines come from this separate pass with HIP events at every "

@@ -8,6 +8,9 @@ row roots, column roots and its data root, from the C oracle
 (oracle/cda_oracle.c, the CPU restatement pinned by the reference's golden
 vectors and mainnet block 408).  `--k 512 --count 2 --out
 tests/golden/k512.json` writes the same for config 3's squares 0 and 1.
+`--first 128 --count 896 --roots-only --out tests/golden/config4_k128_rest.json`
+writes the data root and root digests of the other seven ranks' squares
+(every rank's shard is then checked, not only rank 0's).
 """
 import hashlib
 import json
@@ -35,6 +38,7 @@ def main():
     ap.add_argument("--first", type=int, default=0)
     ap.add_argument("--count", type=int, default=128)
     ap.add_argument("--out", default=os.path.join(GOLDEN, "config4_k128.json"))
+    ap.add_argument("--roots-only", action="store_true", help="data root and root digests only (smaller fixture)")
     a = ap.parse_args()
     first, count, k = a.first, a.count, a.k
     from celestia_da import testfactory   # the bench's generator must agree with the oracle's
@@ -46,9 +50,10 @@ def main():
         if i % 32 == 0 or k > 128:
             assert np.array_equal(ods, testfactory.random_square(k, i))
         eds, rows, cols, root = coracle.cpu_baseline(ods, os.cpu_count() or 8)
-        out["squares"][str(i)] = {"ods_sha256": digest(ods), "eds_sha256": digest(eds),
-                                  "row_roots_sha256": digest(rows), "col_roots_sha256": digest(cols),
-                                  "data_root": root.hex()}
+        rec = {"row_roots_sha256": digest(rows), "col_roots_sha256": digest(cols), "data_root": root.hex()}
+        if not a.roots_only:
+            rec.update(ods_sha256=digest(ods), eds_sha256=digest(eds))
+        out["squares"][str(i)] = rec
     with open(a.out, "w") as f:
         json.dump(out, f, indent=0, sort_keys=True)
     print("wrote", a.out)

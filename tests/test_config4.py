@@ -39,6 +39,53 @@ def test_fixture_covers_rank0_shard():
     assert [str(i) for i in bench.shard(0, 8, 128)] == sorted(g["squares"], key=int)
 
 
+def _fixture_rest():
+    with open(os.path.join(HERE, "golden", "config4_k128_rest.json")) as f:
+        return json.load(f)
+
+
+def test_fixtures_cover_all_1024_squares():
+    """config4_k128.json (rank 0, full digests) + config4_k128_rest.json
+    (ranks 1..7, data roots and root digests) = every square of config 4."""
+    a, b = _fixture(), _fixture_rest()
+    assert b["k"] == 128 and b["first"] == 128 and b["count"] == 896
+    assert sorted(map(int, a["squares"])) + sorted(map(int, b["squares"])) == list(range(1024))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank", [3, 7])
+def test_config4_other_rank_shard_on_gpu(ctx, rank):
+    """Rank g > 0's shard of the 8-GPU config (squares 128g .. 128g+127) in
+    one in-place submission: every data root and every square's row/column
+    roots against the oracle fixture."""
+    import torch
+
+    from celestia_da import testfactory
+    import bench
+    g = _fixture_rest()
+    k, n = 128, 128
+    W = 2 * k
+    idx = list(bench.shard(rank, 8, n))
+    dev = torch.device("cuda", 0)
+    eds = torch.zeros(n, W * W * 512, dtype=torch.uint8, device=dev)
+    for j, i in enumerate(idx):
+        eds[j].view(W, W, 512)[:k, :k] = torch.from_numpy(testfactory.random_square(k, i)).to(dev).view(k, k, 512)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    r, c, dr = rows.cpu().numpy(), cols.cpu().numpy(), roots.cpu().numpy()
+    for j, i in enumerate(idx):
+        want = g["squares"][str(i)]
+        assert dr[j].tobytes().hex() == want["data_root"], i
+        assert _sha(r[j].reshape(W, 90)) == want["row_roots_sha256"], i
+        assert _sha(c[j].reshape(W, 90)) == want["col_roots_sha256"], i
+
+
 def test_shard_partitions_config4():
     import bench
     for world in (1, 2, 4, 8):
