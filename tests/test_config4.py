@@ -7,6 +7,7 @@ sharded across GPUs with no collective.
     fixture tests/golden/config4_k128.json (oracle/gen_config4.py), a sample
     of full EDSs by digest and one square byte-for-byte against the C oracle.
     Reference analogue: the block replay of app/process_proposal.go:138-152.
+    Ranks 3 and 7 (squares 384.. and 896..) against config4_k128_rest.json.
   * CPU (gloo, world size 2): bench.py's rank partition and the MAX-over-ranks
     reduction of its timed region.
 """
