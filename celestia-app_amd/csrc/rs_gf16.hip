@@ -382,7 +382,9 @@ constexpr uint32_t cw_lds_bytes() {
 // Timing-diagnostic builds only (tools/rs16_phase_probe.sh, wrong output):
 // CDA_RS16_PROBE=1 drops the butterfly layers (memory + exchanges alone),
 // =2 drops the global loads and stores (compute + exchanges alone),
-// =3 gives every wave wave 0's pass-A / A' constants (scalar-cache hits).
+// =3 gives every wave wave 0's pass-A / A' constants (scalar-cache hits),
+// =4 stores one dword per lane and parity shard (half the stores),
+// =5 stores no parity (loads kept).
 #ifndef CDA_RS16_PROBE
 #define CDA_RS16_PROBE 0
 #endif
@@ -585,7 +587,14 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
     // parity shard j is stored as soon as its last butterfly is done
     auto store_j = [&](auto jj) {
-        if constexpr (kRs16Memory) st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]);
+        if constexpr (CDA_RS16_PROBE == 4) {   // timing probe: the lo dwords only (half the stores)
+            uint8_t* p = E + d0 + (base + jj.value) * ds;
+            *reinterpret_cast<uint32_t*>(p + off) = lo[jj.value] ^ hi[jj.value];
+        } else if constexpr (CDA_RS16_PROBE == 5) {   // timing probe: no parity stores at all
+            if ((lo[jj.value] ^ hi[jj.value]) == 0x9E3779B9u && threadIdx.x == 1023u) E[d0] = 1;
+        } else if constexpr (kRs16Memory) {
+            st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]);
+        }
     };
     if constexpr (kRs16Compute)
         fft_regs<S>(lo, hi, T, TB + 8 * S * (CDA_RS16_PROBE == 3 ? 0u : wave), [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); },
