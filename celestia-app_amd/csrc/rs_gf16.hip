@@ -306,9 +306,11 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
 #endif
             // the group's operands pass through volatile asm after the load, so
             // the scheduler cannot hoist the butterflies above it
+#ifndef CDA_RS16_NOLAUNDER
             sfor<0, M, 1>([&](auto mm) {
                 launder<N * decltype(mm)::value + g, N * decltype(mm)::value + g + 2 * d>(lo, hi);
             });
+#endif
 #ifdef CDA_RS16_CHUNK2
             uint32_t t[16];
 #pragma unroll
