@@ -555,16 +555,6 @@ hipEvent_t Engine::sync_event(size_t i) {
     return sync_events_[i];
 }
 
-// Batch pipeline.  The batch is cut into chunks of c squares; chunk i's RS
-// extension runs on aux_stream_ and its leaves and wide NMT levels on the
-// caller's stream after an event, so the RS of chunk i+1 (memory-bound: its
-// half-footprint kernel leaves room for hash waves on every CU) runs under the
-// SHA-256 of chunk i (VALU-bound).  The narrow levels, the tree tops and the
-// data roots -- latency-bound -- run once for the whole batch at the end.
-// aux_stream_ starts after the work already queued on `s` and `s` waits for
-// every chunk's RS before hashing it, so the call keeps single-stream
-// semantics for the caller.  Events are re-recorded by later calls only after
-// hipStreamWaitEvent has captured them (HIP semantics).
 // The RS / hash CU partition of CDA_RS_CUS: RS on CUs (33 j) mod ncu, j < N --
 // spread over the XCDs whether the mask bits run XCD-major or CU-major.
 int Engine::make_cu_streams() {
@@ -586,6 +576,16 @@ int Engine::make_cu_streams() {
     return check(hipExtStreamCreateWithCUMask(&hash_cu_stream_, (uint32_t)hs.size(), hs.data()), "cu mask stream");
 }
 
+// Batch pipeline.  The batch is cut into chunks of c squares; chunk i's RS
+// extension runs on aux_stream_ and its leaves and wide NMT levels on the
+// caller's stream after an event, so the RS of chunk i+1 (memory-bound: its
+// half-footprint kernel leaves room for hash waves on every CU) runs under the
+// SHA-256 of chunk i (VALU-bound).  The narrow levels, the tree tops and the
+// data roots -- latency-bound -- run once for the whole batch at the end.
+// aux_stream_ starts after the work already queued on `s` and `s` waits for
+// every chunk's RS before hashing it, so the call keeps single-stream
+// semantics for the caller.  Events are re-recorded by later calls only after
+// hipStreamWaitEvent has captured them (HIP semantics).
 int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                                uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
                                hipStream_t s) {
