@@ -586,7 +586,7 @@ constexpr uint32_t kPairMaxParents = 128;   // 256 lanes: one wave per SIMD of t
 __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
                                                                uint8_t* __restrict__ data_roots,
                                                                const uint32_t* __restrict__ err,
-                                                               int32_t* __restrict__ status) {
+                                                               int32_t* __restrict__ status, uint32_t pair_ok) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [n/2][8] | [n/4][8]
     const size_t sq = blockIdx.x;
     const uint32_t* D = dig + sq * (size_t)n * 8;
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* 
     for (uint32_t m = n / 2; m >= 1; m >>= 1) {
         const uint32_t* in = m == n / 2 ? D : src;
         uint32_t* out = m == n / 2 ? src : dst;
-        if (m <= kPairMaxParents && 2 * m <= blockDim.x)
+        if (pair_ok && m <= kPairMaxParents && 2 * m <= blockDim.x)
             data_root_level<true>(in, out, m);
         else
             data_root_level<false>(in, out, m);
@@ -710,6 +710,16 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
     return hipGetLastError();
 }
 
+// CDA_TOP_PAIR=0 (A/B knob): one thread per parent in the tree tops and the
+// data root instead of the lane-pair compression.
+static bool pair_sha_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("CDA_TOP_PAIR");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint32_t* dig,
                            uint32_t n_items, hipStream_t s, uint32_t* n_dig_out) {
     if (n_forest < 1 || n_forest > 2 || n_in < 2 || n_in > 2 * kTopThreads || (n_in & (n_in - 1)))
@@ -727,12 +737,16 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
     uint32_t lv = 0;
     if (dig && trees == n_items && (n_items & (n_items - 1)) == 0 && tpw <= n_items)
         while ((2u << lv) <= tpw && (n_items >> (lv + 1)) >= 2) lv++;
-    if (getenv("CDA_TOP_RFC") && atoi(getenv("CDA_TOP_RFC")) == 0) lv = 0;
+    static const bool rfc_in_top = [] {   // CDA_TOP_RFC=0: leaf digests only (A/B knob)
+        const char* e = getenv("CDA_TOP_RFC");
+        return !(e && atoi(e) == 0);
+    }();
+    if (!rfc_in_top) lv = 0;
     const uint32_t n_dig = n_items >> lv;
     if (n_dig_out) *n_dig_out = n_dig;
     // lane pairs while they still fit in a wave per SIMD (1024 SIMDs)
     const uint64_t parents = (uint64_t)n * trees * (n_in / 2);
-    const bool pair = 2 * parents <= 65536 && !(getenv("CDA_TOP_PAIR") && atoi(getenv("CDA_TOP_PAIR")) == 0);
+    const bool pair = pair_sha_enabled() && 2 * parents <= 65536;
     const dim3 grid((trees + tpw - 1) / tpw, n);
     if (pair)
         hipLaunchKernelGGL(tree_top_kernel<true>, grid, dim3(2 * kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv);
@@ -785,7 +799,7 @@ hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint3
     threads = std::max<uint32_t>(threads, std::min<uint32_t>(n_items, 2 * kPairMaxParents));
     threads = std::max<uint32_t>((threads + 63) / 64 * 64, 64);
     hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots,
-                       status ? err : nullptr, status);
+                       status ? err : nullptr, status, pair_sha_enabled() ? 1u : 0u);
     return hipGetLastError();
 }
 
