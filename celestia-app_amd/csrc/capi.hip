@@ -400,7 +400,7 @@ int cda_blob_commitments(cda_ctx* ctx, const uint8_t* namespaces, const uint8_t*
         if (n == 0) return CDA_OK;
         if (!namespaces || !data_off || !commitments || (data_off[n] > data_off[0] && !data))
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        cda::square::CommitPlan p;
+        cda::square::CommitPlan& p = e.commit_plan();
         std::string err;
         if (cda::square::plan_commitments(namespaces, data_off, share_versions, n, threshold, &p, &err))
             return e.fail(CDA_ERR_SQUARE, err);
@@ -415,7 +415,7 @@ int cda_blob_commitments_device(cda_ctx* ctx, const uint8_t* namespaces, const u
         if (n == 0) return CDA_OK;
         if (!namespaces || !data_off || !d_commitments || (data_off[n] > data_off[0] && !d_data))
             return e.fail(CDA_ERR_INVALID, "null buffer");
-        cda::square::CommitPlan p;
+        cda::square::CommitPlan& p = e.commit_plan();
         std::string err;
         if (cda::square::plan_commitments(namespaces, data_off, share_versions, n, threshold, &p, &err))
             return e.fail(CDA_ERR_SQUARE, err);

@@ -166,11 +166,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
 }
 
 // Per-leaf segment and subtree index tables, built on the device from the
-// plan's segment and subtree lists (binary search per leaf) instead of
-// shipping 8 bytes per leaf over PCIe.
+// plan's segment list (binary search per leaf) instead of shipping 8 bytes per
+// leaf over PCIe.  The subtree list is written here too: a blob's subtrees
+// (inclusion.MerkleMountainRangeSizes: n >> sub_log full ones, then one per
+// set bit of the remainder r, largest first) follow from its segment, and the
+// first leaf of each subtree writes its record.  A remainder leaf j lies in
+// the subtree of the highest bit where j and r differ (r has it set).
 __global__ __launch_bounds__(256) void leaf_tables_kernel(const square::Segment* __restrict__ segs, uint32_t n_segs,
-                                                          const Tree* __restrict__ trees, uint32_t n_trees,
-                                                          uint32_t* __restrict__ leaf_seg,
+                                                          const uint32_t* __restrict__ seg_tree0,
+                                                          Tree* __restrict__ trees, uint32_t* __restrict__ leaf_seg,
                                                           uint32_t* __restrict__ leaf_tree, uint32_t n_leaves) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n_leaves) return;
@@ -181,14 +185,26 @@ __global__ __launch_bounds__(256) void leaf_tables_kernel(const square::Segment*
         else hi = mid;
     }
     leaf_seg[i] = lo;
-    lo = 0;
-    hi = n_trees;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (trees[mid].off <= i) lo = mid;
-        else hi = mid;
+    const uint32_t t0 = seg_tree0[lo];
+    const square::Segment* g = segs + lo;
+    if (t0 == square::kNoTree || g->kind != square::kSegBlob) {
+        leaf_tree[i] = square::kNoTree;
+        return;
     }
-    leaf_tree[i] = lo;
+    const uint32_t j = i - g->start, wl = g->sub_log, full = g->n >> wl;
+    uint32_t q, off, h;
+    if ((j >> wl) < full) {
+        q = j >> wl;
+        off = q << wl;
+        h = wl;
+    } else {
+        const uint32_t base = full << wl, r = g->n - base, jr = j - base;
+        h = 31u - (uint32_t)__builtin_clz(r ^ jr);
+        q = full + (uint32_t)__builtin_popcount(r >> (h + 1));
+        off = base + (r & ~((2u << h) - 1));
+    }
+    leaf_tree[i] = t0 + q;
+    if (j == off) trees[t0 + q] = Tree{g->start + off, h};
 }
 
 // Height-0 subtrees (single share): the root is the leaf node itself.
@@ -210,7 +226,8 @@ __global__ __launch_bounds__(256) void subtree_level_kernel(const Tree* __restri
     const uint32_t n = blockIdx.x * 256 + threadIdx.x;
     if (n >= n_nodes) return;
     const uint32_t leaf0 = n << level;
-    const uint32_t lo = leaf_tree[leaf0];   // last subtree with off <= leaf0
+    const uint32_t lo = leaf_tree[leaf0];   // subtree holding leaf0 (kNoTree: alignment gap)
+    if (lo == square::kNoTree) return;
     const Tree T = trees[lo];
     if (T.off > leaf0 || T.height < level || leaf0 - T.off >= (1u << T.height)) return;
     uint32_t L[kSlotWords], R[kSlotWords], w[16];
@@ -277,7 +294,27 @@ __global__ __launch_bounds__(64) void commitment_kernel(const uint32_t* __restri
     __syncthreads();
     while (m > 1) {
         const uint32_t pairs = m / 2;
-        for (uint32_t i = threadIdx.x; i < pairs; i += blockDim.x) rfc_inner(src + 16 * i, src + 16 * i + 8, dst + 8 * i);
+        if (2 * pairs <= blockDim.x) {
+            // a lane pair per parent (sha_pair_compress): the narrow levels
+            // of the per-blob chain are latency-bound
+            const uint32_t i = threadIdx.x >> 1;
+            const bool A = threadIdx.x & 1;
+            if (i < pairs) {
+                uint32_t a[8], bb[8], D[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    a[j] = src[16 * i + j];
+                    bb[j] = src[16 * i + 8 + j];
+                }
+                rfc_inner_u<true>(a, bb, D, A);
+                if (!A) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) dst[8 * i + j] = D[j];
+                }
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < pairs; i += blockDim.x) rfc_inner(src + 16 * i, src + 16 * i + 8, dst + 8 * i);
+        }
         if ((m & 1) && threadIdx.x < 8) dst[pairs * 8 + threadIdx.x] = src[(m - 1) * 8 + threadIdx.x];
         __syncthreads();
         uint32_t* t = src;
@@ -325,9 +362,9 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
                                 hipStream_t s) {
     if (n_blobs == 0) return CDA_OK;
     const size_t seg_b = p.segs.size() * sizeof(square::Segment);
-    const size_t tree_b = p.trees.size() * sizeof(Tree);
+    const size_t st_b = p.seg_tree0.size() * 4;
     const size_t bt_b = p.blob_tree0.size() * 4;
-    const size_t plan_b = seg_b + tree_b + bt_b;
+    const size_t plan_b = seg_b + st_b + bt_b;
     int rc;
     if (sq_event_ && (rc = check(hipEventSynchronize(sq_event_), "hipEventSynchronize"))) return rc;
     if (plan_b > sq_stage_bytes_) {
@@ -341,24 +378,25 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
         return rc;
     uint8_t* stage = static_cast<uint8_t*>(sq_stage_);
     if (seg_b) std::memcpy(stage, p.segs.data(), seg_b);
-    if (tree_b) std::memcpy(stage + seg_b, p.trees.data(), tree_b);
-    std::memcpy(stage + seg_b + tree_b, p.blob_tree0.data(), bt_b);
+    if (st_b) std::memcpy(stage + seg_b, p.seg_tree0.data(), st_b);
+    std::memcpy(stage + seg_b + st_b, p.blob_tree0.data(), bt_b);
     if ((rc = check(cm_plan_.ensure(plan_b), "hipMalloc"))) return rc;
     if ((rc = check(hipMemcpyAsync(cm_plan_.ptr, stage, plan_b, hipMemcpyHostToDevice, s), "H2D plan"))) return rc;
     if ((rc = check(hipEventRecord(sq_event_, s), "hipEventRecord"))) return rc;
     const square::Segment* d_segs = cm_plan_.as<square::Segment>();
-    const Tree* d_trees = reinterpret_cast<const Tree*>(cm_plan_.as<uint8_t>() + seg_b);
-    const uint32_t* d_bt = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b + tree_b);
-    const uint32_t N = p.n_leaves, n_trees = (uint32_t)p.trees.size();
+    const uint32_t* d_st = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b);
+    const uint32_t* d_bt = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b + st_b);
+    const uint32_t N = p.n_leaves, n_trees = p.n_trees;
     if (N) {
         if ((rc = check(cm_leaf_.ensure((size_t)N * kSlot), "hipMalloc"))) return rc;
         if ((rc = check(cm_lvl_.ensure((size_t)(N / 2 + 1) * kSlot), "hipMalloc"))) return rc;
         if ((rc = check(cm_roots_.ensure((size_t)n_trees * 32), "hipMalloc"))) return rc;   // RFC leaf digests
-        if ((rc = check(cm_tables_.ensure((size_t)N * 8), "hipMalloc"))) return rc;
+        if ((rc = check(cm_tables_.ensure((size_t)N * 8 + (size_t)n_trees * sizeof(Tree)), "hipMalloc"))) return rc;
         uint32_t* d_leaf_seg = cm_tables_.as<uint32_t>();
         uint32_t* d_leaf_tree = d_leaf_seg + N;
+        Tree* d_trees = reinterpret_cast<Tree*>(d_leaf_tree + N);
         hipLaunchKernelGGL(leaf_tables_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, (uint32_t)p.segs.size(),
-                           d_trees, n_trees, d_leaf_seg, d_leaf_tree, N);
+                           d_st, d_trees, d_leaf_seg, d_leaf_tree, N);
         if ((rc = check(hipGetLastError(), "leaf tables"))) return rc;
         hipLaunchKernelGGL(blob_leaf_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, d_leaf_seg, d_data,
                            cm_leaf_.as<uint8_t>(), N);

@@ -167,6 +167,9 @@ class Engine {
 
     // Blob share commitments (commit.hip).  d_data: blob bytes the plan's
     // offsets refer to (>= 16 readable bytes of slack); d_out: n_blobs * 32.
+    // Host plan reused by every commitment call (its vectors keep their
+    // capacity; the engine mutex serialises callers).
+    square::CommitPlan& commit_plan() { return cm_host_plan_; }
     int enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* d_data, uint8_t* d_out,
                             hipStream_t s);
     int host_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* data, size_t data_len,
@@ -290,6 +293,7 @@ class Engine {
     // copy of host txs, pinned staging for the plan and its copy-done event
     DevBuf sq_plan_, sq_txs_;
     DevBuf cm_plan_, cm_tables_, cm_leaf_, cm_lvl_, cm_roots_, cm_out_;   // commitments
+    square::CommitPlan cm_host_plan_;
     void* sq_stage_ = nullptr;
     size_t sq_stage_bytes_ = 0;
     hipEvent_t sq_event_ = nullptr;

@@ -306,31 +306,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
     }
 }
 
-// ---------------------------------------------------------------------------
-// SHA-256 of one unit: a thread (PAIR = false) or a lane pair (PAIR = true,
-// sha_pair_compress: the latency-bound tails, where a wave per SIMD or fewer
-// is all the work there is).  Every message word is computed by both lanes.
-// ---------------------------------------------------------------------------
-template <bool PAIR>
-struct Sha;
-template <>
-struct Sha<false> {
-    ShaState st;
-    __device__ __forceinline__ void init(bool) { sha_init(st); }
-    __device__ __forceinline__ void compress(uint32_t (&w)[16], bool) { sha_compress(st, w); }
-    __device__ __forceinline__ void digest(bool, uint32_t (&d)[8]) const {
-#pragma unroll
-        for (int j = 0; j < 8; j++) d[j] = st.h[j];
-    }
-};
-template <>
-struct Sha<true> {
-    ShaPair st;
-    __device__ __forceinline__ void init(bool A) { sha_pair_init(st, A); }
-    __device__ __forceinline__ void compress(uint32_t (&w)[16], bool A) { sha_pair_compress(st, w, A); }
-    __device__ __forceinline__ void digest(bool A, uint32_t (&d)[8]) const { sha_pair_digest(st, A, d); }
-};
-
 // HashNode (no mid-state branch: the tails mix data- and parity-left parents).
 template <bool PAIR>
 __device__ __forceinline__ void hash_node_u(const uint32_t (&L)[kSlotWords], const uint32_t (&R)[kSlotWords],
@@ -347,35 +322,6 @@ __device__ __forceinline__ void hash_node_u(const uint32_t (&L)[kSlotWords], con
     h.digest(A, D);
     inner_node_words(L, R, D, o);
 }
-// RFC-6962 leaf digest sha256(0x00 || slot[0:90]); I = big-endian slot words.
-template <bool PAIR>
-__device__ __forceinline__ void rfc_leaf_u(const uint32_t (&I)[kSlotWords], uint32_t (&D)[8], bool A) {
-    Sha<PAIR> h;
-    h.init(A);
-    uint32_t w[16];
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
-        h.compress(w, A);
-    }
-    h.digest(A, D);
-}
-// RFC-6962 inner digest sha256(0x01 || a || b) of two digests.
-template <bool PAIR>
-__device__ __forceinline__ void rfc_inner_u(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&D)[8], bool A) {
-    Sha<PAIR> h;
-    h.init(A);
-    uint32_t w[16];
-#pragma unroll
-    for (int blk = 0; blk < 2; blk++) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(a, b, 16 * blk + j);
-        h.compress(w, A);
-    }
-    h.digest(A, D);
-}
-
 // ---------------------------------------------------------------------------
 // Fused top of the trees (latency-bound part: fewer parents than the chip has
 // wave slots).  One workgroup takes tpw trees and runs every remaining level

@@ -589,15 +589,20 @@ int plan(const uint8_t* txs, const uint64_t* off, uint32_t n, uint32_t max_ss, u
 int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const uint8_t* share_versions, uint32_t n,
                      uint32_t threshold, CommitPlan* out, std::string* err) {
     CommitPlan& P = *out;
-    P = CommitPlan{};
+    P.n_leaves = P.max_height = P.max_trees = P.n_trees = 0;
+    P.segs.clear();
+    P.seg_tree0.clear();
+    P.blob_tree0.clear();
     if (threshold == 0) {
         *err = "subtree root threshold must be positive";
         return -1;
     }
     P.blob_tree0.reserve(n + 1);
+    P.segs.reserve(2 * (size_t)n);
+    P.seg_tree0.reserve(2 * (size_t)n);
     uint64_t cursor = 0;
     for (uint32_t b = 0; b < n; b++) {
-        P.blob_tree0.push_back((uint32_t)P.trees.size());
+        P.blob_tree0.push_back(P.n_trees);
         const uint8_t* ns = namespaces + (size_t)b * kNs;
         const uint8_t ver = share_versions ? share_versions[b] : 0;
         if (ver != 0) {
@@ -635,6 +640,7 @@ int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const 
             g.start = (uint32_t)cursor;
             g.n = (uint32_t)(start - cursor);
             P.segs.push_back(g);
+            P.seg_tree0.push_back(kNoTree);
         }
         Segment s{};
         s.kind = kSegBlob;
@@ -644,22 +650,15 @@ int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const 
         s.src = data_off[b];
         s.len = (uint32_t)len;
         std::memcpy(s.ns, ns, kNs);
+        uint32_t sub_log = 0;
+        while ((1u << sub_log) < w) sub_log++;
+        s.sub_log = (uint8_t)sub_log;
         P.segs.push_back(s);
-        uint32_t left = n_sh, off = (uint32_t)start, nt = 0;
-        while (left) {   // inclusion.MerkleMountainRangeSizes
-            uint32_t size = w;
-            if (left < w) {
-                size = 1;
-                while (size * 2 <= left) size *= 2;
-            }
-            uint32_t h = 0;
-            while ((1u << h) < size) h++;
-            P.trees.push_back(Tree{off, h});
-            P.max_height = std::max(P.max_height, h);
-            off += size;
-            left -= size;
-            nt++;
-        }
+        P.seg_tree0.push_back(P.n_trees);
+        const uint32_t nt = mmr_tree_count(n_sh, sub_log);   // inclusion.MerkleMountainRangeSizes
+        const uint32_t top = (n_sh >> sub_log) ? sub_log : 31u - (uint32_t)__builtin_clz(n_sh);
+        P.max_height = std::max(P.max_height, top);
+        P.n_trees += nt;
         P.max_trees = std::max(P.max_trees, nt);
         cursor = start + n_sh;
         if (cursor > 0x7FFFFFFFull) {
@@ -667,7 +666,7 @@ int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const 
             return -1;
         }
     }
-    P.blob_tree0.push_back((uint32_t)P.trees.size());
+    P.blob_tree0.push_back(P.n_trees);
     P.n_leaves = (uint32_t)cursor;
     return 0;
 }

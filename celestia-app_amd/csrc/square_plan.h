@@ -42,7 +42,8 @@ struct Segment {
     uint64_t src;          // kSegCompact: byte offset in the compact buffer; kSegBlob: byte offset of the blob data in the tx buffer
     uint32_t len;          // kSegBlob: blob data length (sequence length)
     uint8_t ns[kNs];       // namespace (kSegPadding / kSegBlob)
-    uint8_t pad_[7];
+    uint8_t sub_log;       // CommitPlan kSegBlob: log2(subtree width)
+    uint8_t pad_[6];
 };
 static_assert(sizeof(Segment) == 64, "Segment is 64 bytes");
 
@@ -75,16 +76,28 @@ struct Tree {
     uint32_t off;      // first leaf (multiple of 1 << height)
     uint32_t height;   // log2(size)
 };
+// The subtree list itself (n_trees Tree records, blob order then MMR order) is
+// not built here: it follows from each blob segment's start, share count and
+// sub_log, and the device writes it (commit.hip leaf_tables_kernel).
+constexpr uint32_t kNoTree = 0xFFFFFFFFu;
 struct CommitPlan {
     uint32_t n_leaves = 0;             // leaf array length (blobs + alignment gaps)
     uint32_t max_height = 0;
     uint32_t max_trees = 0;            // most subtree roots of one blob
+    uint32_t n_trees = 0;              // all subtrees of all blobs
     std::vector<Segment> segs;         // share layout of the leaf array (blob segments + gaps)
-    std::vector<Tree> trees;           // all subtrees, blob order then MMR order
+    std::vector<uint32_t> seg_tree0;   // first tree of each segment's blob (kNoTree for gaps)
     std::vector<uint32_t> blob_tree0;  // first tree of blob i (n + 1 entries: prefix sums)
 };
+// Subtrees of a blob of n shares with width 1 << sub_log
+// (inclusion.MerkleMountainRangeSizes): n >> sub_log of full width, then one per
+// set bit of the remainder, largest first.
+inline uint32_t mmr_tree_count(uint32_t n, uint32_t sub_log) {
+    return (n >> sub_log) + (uint32_t)__builtin_popcount(n & ((1u << sub_log) - 1));
+}
 // namespaces: n * 29 bytes; data_off: n + 1 offsets into the blob data;
-// share_versions: n bytes or NULL (all 0).
+// share_versions: n bytes or NULL (all 0).  *out is reused: its vectors keep
+// their capacity from call to call.
 int plan_commitments(const uint8_t* namespaces, const uint64_t* data_off, const uint8_t* share_versions, uint32_t n,
                      uint32_t threshold, CommitPlan* out, std::string* err);
 
