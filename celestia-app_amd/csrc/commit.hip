@@ -27,7 +27,10 @@
 //      those digests in LDS (odd nodes promoted, equal to the RFC split rule).
 // VALU-bound like the EDS hashing: 9 compressions per share + 3 per inner node
 // + 2 per subtree root and RFC node.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../include/cda.h"
 #include "engine.h"
@@ -98,10 +101,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     const uint32_t A0 = (uint32_t)(B >> 2);
     const uint32_t last = (uint32_t)(((int64_t)B + L - 1) >> 2);   // L >= -3 and B >= 4 when L <= 0
     const uint32_t* D = reinterpret_cast<const uint32_t*>(data);
+    // one 16-byte load per chunk (dword-aligned: global loads need only
+    // dword alignment), not four dword loads -- a lane's chunks lie in its
+    // own share, so each load instruction touches 64 distinct cache lines
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
     auto chunk = [&](uint32_t dw, uint32_t* x) {
         dw = min(dw, last);
-#pragma unroll
-        for (int q = 0; q < 4; q++) x[q] = D[dw + q];
+        const u32x4a v = *reinterpret_cast<const u32x4a*>(D + dw);
+        x[0] = v.x;
+        x[1] = v.y;
+        x[2] = v.z;
+        x[3] = v.w;
     };
 
     uint32_t N[8];
@@ -328,6 +338,125 @@ __global__ __launch_bounds__(64) void commitment_kernel(const uint32_t* __restri
     }
 }
 
+// Blob groups: one wave takes the consecutive blobs [group_blob0[g],
+// group_blob0[g + 1]) (at most 64) and runs their RFC-6962 levels together:
+// each level's parents of all the group's blobs are one flat list of units
+// over the wave's lanes (a lane pair per unit when they fit, else a lane per
+// unit), so the narrow upper levels of one blob share the wave's instruction
+// stream with those of its neighbours instead of idling 60 of 64 lanes.  The
+// digests stay in LDS, each blob's level compacted in place at the front of
+// its own slot range (every unit reads its two children before any unit
+// writes; the odd node is promoted after the level's writes).
+__global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __restrict__ dig,
+                                                               const uint32_t* __restrict__ blob_tree0,
+                                                               const uint32_t* __restrict__ group_blob0,
+                                                               uint8_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [group trees][8]
+    __shared__ uint32_t pre[64], bbase[64];
+    const uint32_t b0 = group_blob0[blockIdx.x], G = group_blob0[blockIdx.x + 1] - b0;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t t_base = blob_tree0[b0], T = blob_tree0[b0 + G] - t_base;
+    for (uint32_t i = lane; i < T * 8; i += 64) hs[i] = dig[(size_t)t_base * 8 + i];
+    uint32_t m = 0, base = 0;
+    if (lane < G) {
+        base = blob_tree0[b0 + lane] - t_base;
+        m = blob_tree0[b0 + lane + 1] - blob_tree0[b0 + lane];
+        bbase[lane] = base;
+    }
+    __syncthreads();
+    // blob of unit u: the first i with pre[i] > u (pre = inclusive prefix of
+    // the level's parent counts)
+    auto find = [&](uint32_t u) {
+        if (G == 1) return 0u;
+        uint32_t lo = 0, hi = G - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] > u) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    };
+    for (;;) {
+        const uint32_t p = m / 2;
+        uint32_t sc = p;
+#pragma unroll
+        for (int k = 1; k < 64; k <<= 1) {
+            const uint32_t v = __shfl_up(sc, k, 64);
+            if (lane >= (uint32_t)k) sc += v;
+        }
+        const uint32_t total = __shfl(sc, 63, 64);
+        if (total == 0) break;
+        pre[lane] = sc;
+        const bool odd = (m & 1) && m > 1;
+        uint32_t carry[8];
+        if (odd) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) carry[j] = hs[(base + m - 1) * 8 + j];
+        }
+        __syncthreads();
+        if (2 * total <= 64) {
+            const uint32_t u = lane >> 1;
+            const bool A = lane & 1;
+            uint32_t D[8], slot = 0;
+            if (u < total) {
+                const uint32_t i = find(u);
+                const uint32_t q = u - (i ? pre[i - 1] : 0u);
+                const uint32_t c = (bbase[i] + 2 * q) * 8;
+                uint32_t a[8], bb[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    a[j] = hs[c + j];
+                    bb[j] = hs[c + 8 + j];
+                }
+                rfc_inner_u<true>(a, bb, D, A);
+                slot = (bbase[i] + q) * 8;
+            }
+            __syncthreads();
+            if (u < total && !A) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) hs[slot + j] = D[j];
+            }
+        } else {
+            // a later pass's children lie past every slot an earlier pass wrote
+            for (uint32_t u0 = 0; u0 < total; u0 += 64) {
+                const uint32_t u = u0 + lane;
+                uint32_t D[8], slot = 0;
+                if (u < total) {
+                    const uint32_t i = find(u);
+                    const uint32_t q = u - (i ? pre[i - 1] : 0u);
+                    const uint32_t c = (bbase[i] + 2 * q) * 8;
+                    rfc_inner(hs + c, hs + c + 8, D);
+                    slot = (bbase[i] + q) * 8;
+                }
+                __syncthreads();
+                if (u < total) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) hs[slot + j] = D[j];
+                }
+            }
+        }
+        __syncthreads();
+        if (odd) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) hs[(base + p) * 8 + j] = carry[j];
+        }
+        m = p + (m & 1);
+        __syncthreads();
+    }
+    if (lane < G) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + (size_t)(b0 + lane) * 32);
+        if (m == 0) {   // no shares: merkle.HashFromByteSlices(nil) = sha256("")
+            const uint32_t e[8] = {0x42c4b0e3u, 0x141cfc98u, 0xc8f4fb9au, 0x24b96f99u,
+                                   0xe441ae27u, 0x4c939b64u, 0x1b9995a4u, 0x55b85278u};
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = e[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) o[j] = bswap32(hs[base * 8 + j]);
+        }
+    }
+}
+
 // RFC-6962 leaf digests of n 96-B slots.
 __global__ __launch_bounds__(256) void slot_digest_kernel(const uint8_t* __restrict__ slots, uint32_t n,
                                                           uint32_t* __restrict__ dig) {
@@ -358,13 +487,57 @@ hipError_t launch_slot_merkle_roots(const uint8_t* slots, const uint32_t* bt, ui
 // ---------------------------------------------------------------------------
 // Engine glue
 // ---------------------------------------------------------------------------
+// CDA_COMMIT_GROUP=0: one wave per blob (commitment_kernel) instead of blob
+// groups (A/B knob, read once).
+static bool group_commitments() {
+    static const bool on = [] {
+        const char* e = std::getenv("CDA_COMMIT_GROUP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* d_data, uint8_t* d_out,
                                 hipStream_t s) {
     if (n_blobs == 0) return CDA_OK;
     const size_t seg_b = p.segs.size() * sizeof(square::Segment);
     const size_t st_b = p.seg_tree0.size() * 4;
     const size_t bt_b = p.blob_tree0.size() * 4;
-    const size_t plan_b = seg_b + st_b + bt_b;
+    // Blob groups for commitment_group_kernel: consecutive blobs while the
+    // group's first-level parents stay within ucap units -- 32 (one lane pair
+    // each) for a small batch, enough for about one group per SIMD for a large
+    // one -- and its subtree roots within tcap LDS slots.
+    std::vector<uint32_t>& grp = cm_groups_;
+    grp.clear();
+    uint32_t max_gt = 0;
+    if (group_commitments()) {
+        const uint32_t* bt = p.blob_tree0.data();
+        uint64_t units = 0;
+        for (uint32_t b = 0; b < n_blobs; b++) units += (bt[b + 1] - bt[b]) / 2;
+        // CDA_COMMIT_UCAP (read per call; tests): a larger minimum, to drive
+        // the lane-per-unit passes with small batches
+        const char* ue = std::getenv("CDA_COMMIT_UCAP");
+        const uint64_t umin = ue ? std::max(1L, std::atol(ue)) : 32;
+        const uint32_t ucap = (uint32_t)std::max<uint64_t>(umin, (units + 1023) / 1024);
+        const uint32_t tcap = std::max(p.max_trees, 512u);
+        uint32_t g0 = 0, gu = 0, gt = 0;
+        grp.push_back(0);
+        for (uint32_t b = 0; b < n_blobs; b++) {
+            const uint32_t nt = bt[b + 1] - bt[b];
+            if (b > g0 && (b - g0 == 64 || gu + nt / 2 > ucap || gt + nt > tcap)) {
+                grp.push_back(b);
+                max_gt = std::max(max_gt, gt);
+                g0 = b;
+                gu = gt = 0;
+            }
+            gu += nt / 2;
+            gt += nt;
+        }
+        grp.push_back(n_blobs);
+        max_gt = std::max(max_gt, gt);
+    }
+    const size_t gr_b = grp.size() * 4;
+    const size_t plan_b = seg_b + st_b + bt_b + gr_b;
     int rc;
     if (sq_event_ && (rc = check(hipEventSynchronize(sq_event_), "hipEventSynchronize"))) return rc;
     if (plan_b > sq_stage_bytes_) {
@@ -380,12 +553,14 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
     if (seg_b) std::memcpy(stage, p.segs.data(), seg_b);
     if (st_b) std::memcpy(stage + seg_b, p.seg_tree0.data(), st_b);
     std::memcpy(stage + seg_b + st_b, p.blob_tree0.data(), bt_b);
+    if (gr_b) std::memcpy(stage + seg_b + st_b + bt_b, grp.data(), gr_b);
     if ((rc = check(cm_plan_.ensure(plan_b), "hipMalloc"))) return rc;
     if ((rc = check(hipMemcpyAsync(cm_plan_.ptr, stage, plan_b, hipMemcpyHostToDevice, s), "H2D plan"))) return rc;
     if ((rc = check(hipEventRecord(sq_event_, s), "hipEventRecord"))) return rc;
     const square::Segment* d_segs = cm_plan_.as<square::Segment>();
     const uint32_t* d_st = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b);
     const uint32_t* d_bt = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b + st_b);
+    const uint32_t* d_grp = reinterpret_cast<const uint32_t*>(cm_plan_.as<uint8_t>() + seg_b + st_b + bt_b);
     const uint32_t N = p.n_leaves, n_trees = p.n_trees;
     if (N) {
         if ((rc = check(cm_leaf_.ensure((size_t)N * kSlot), "hipMalloc"))) return rc;
@@ -412,6 +587,18 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
                                d_leaf_tree, in, out, cm_roots_.as<uint32_t>(), L, n_nodes);
             if ((rc = check(hipGetLastError(), "subtree level"))) return rc;
         }
+    }
+    if (!grp.empty()) {
+        const size_t lds = (size_t)std::max(max_gt, 1u) * 32;
+        if (lds > 159 * 1024) return fail(CDA_ERR_UNSUPPORTED, "too many subtree roots in one blob");
+        if (lds > 64 * 1024 &&
+            (rc = check(hipFuncSetAttribute(reinterpret_cast<const void*>(commitment_group_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                        "hipFuncSetAttribute")))
+            return rc;
+        hipLaunchKernelGGL(commitment_group_kernel, dim3((uint32_t)grp.size() - 1), dim3(64), lds, s,
+                           cm_roots_.as<uint32_t>(), d_bt, d_grp, d_out);
+        return check(hipGetLastError(), "commitments");
     }
     const uint32_t mt = p.max_trees ? p.max_trees : 1;
     const size_t lds = (size_t)(mt + (mt + 1) / 2) * 32;

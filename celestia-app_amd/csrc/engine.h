@@ -294,6 +294,7 @@ class Engine {
     DevBuf sq_plan_, sq_txs_;
     DevBuf cm_plan_, cm_tables_, cm_leaf_, cm_lvl_, cm_roots_, cm_out_;   // commitments
     square::CommitPlan cm_host_plan_;
+    std::vector<uint32_t> cm_groups_;   // commitment blob groups (host side)
     void* sq_stage_ = nullptr;
     size_t sq_stage_bytes_ = 0;
     hipEvent_t sq_event_ = nullptr;

@@ -95,6 +95,23 @@ def test_commitments_batch_many_small_gpu(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ucap", ["1", "100", "1000"])
+def test_commitments_blob_groups_gpu(ctx, ucap, monkeypatch):
+    """commit.hip commitment_group_kernel with forced group sizes: one blob per
+    wave (ucap 1), groups whose levels take lane pairs and single lanes, and
+    groups of up to 64 blobs whose first levels take several passes of the
+    wave (ucap 1000), including empty and one-share blobs."""
+    monkeypatch.setenv("CDA_COMMIT_UCAP", ucap)
+    rng = np.random.default_rng(21)
+    sizes = [int(x) for x in rng.integers(1, 60_000, 150)] + [0, 1, 478, 0] + [int(x) for x in rng.integers(1, 900, 40)]
+    blobs = random_blobs(21, sizes)
+    for threshold in (64, 2):
+        got = ginc.create_commitments(blobs, threshold)
+        for b, c in zip(blobs, got):
+            assert c == oinc.create_commitment(b.namespace, b.data, 0, threshold), (len(b.data), threshold)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("threshold", [1, 8, 128])
 def test_commitments_other_thresholds_gpu(ctx, threshold):
     blobs = random_blobs(11, [1, 500, 7000, 50_000])
