@@ -13,18 +13,22 @@
 // plan_commitments):
 //   1. every blob's sparse shares get leaf positions in one array, blob starts
 //      aligned to their w, so all subtrees are perfect trees aligned to their
-//      size;
-//   2. blob_leaf_kernel hashes every leaf (9 SHA-256 blocks of
-//      0x00 || ns || share -- the same leaves as the EDS Q0 cells), building
-//      the share words straight from the blob bytes (no share copy in HBM);
+//      size; the host sends only the segment list (no per-subtree records);
+//   2. blob_leaf_kernel finds each leaf's segment and subtree (and the first
+//      leaf of each subtree writes the subtree record), then hashes the leaf
+//      (9 SHA-256 blocks of 0x00 || ns || share -- the same leaves as the EDS
+//      Q0 cells), building the share words straight from the blob bytes (no
+//      share copy in HBM);
 //   3. one subtree_level_kernel launch per level for ALL subtrees of ALL
 //      blobs: node n of level L covers leaves [n << L, (n + 1) << L); the
 //      per-leaf subtree table tells whether it lies inside a subtree tall
 //      enough (else the thread exits).
 //      A subtree's top node is hashed straight into its RFC-6962 leaf digest
-//      sha256(0x00 || root) (parallel, off the per-blob serial chain);
-//   4. commitment_kernel: one workgroup per blob, RFC-6962 inner levels over
-//      those digests in LDS (odd nodes promoted, equal to the RFC split rule).
+//      sha256(0x00 || root) (parallel, off the per-blob serial chain); the
+//      level-1 launch also does this for the single-share subtrees;
+//   4. commitment_group_kernel: one wave per group of consecutive blobs,
+//      RFC-6962 inner levels over those digests in LDS (odd nodes promoted,
+//      equal to the RFC split rule).
 // VALU-bound like the EDS hashing: 9 compressions per share + 3 per inner node
 // + 2 per subtree root and RFC node.
 #include <algorithm>
@@ -61,6 +65,45 @@ __device__ __forceinline__ void store_rfc_leaf(const uint32_t (&I)[kSlotWords], 
     d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
 }
 
+// Per-leaf subtree index and the subtree list, built on the device from the
+// plan's segment list (binary search per leaf, at the start of
+// blob_leaf_kernel) instead of shipped over PCIe.  The subtree list is written here too: a blob's subtrees
+// (inclusion.MerkleMountainRangeSizes: n >> sub_log full ones, then one per
+// set bit of the remainder r, largest first) follow from its segment, and the
+// first leaf of each subtree writes its record.  A remainder leaf j lies in
+// the subtree of the highest bit where j and r differ (r has it set).
+__device__ __forceinline__ uint32_t leaf_tables(uint32_t i, const square::Segment* __restrict__ segs, uint32_t n_segs,
+                                                const uint32_t* __restrict__ seg_tree0, Tree* __restrict__ trees,
+                                                uint32_t* __restrict__ leaf_tree) {
+    uint32_t lo = 0, hi = n_segs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segs[mid].start <= i) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t t0 = seg_tree0[lo];
+    const square::Segment* g = segs + lo;
+    if (t0 == square::kNoTree || g->kind != square::kSegBlob) {
+        leaf_tree[i] = square::kNoTree;
+        return lo;
+    }
+    const uint32_t j = i - g->start, wl = g->sub_log, full = g->n >> wl;
+    uint32_t q, off, h;
+    if ((j >> wl) < full) {
+        q = j >> wl;
+        off = q << wl;
+        h = wl;
+    } else {
+        const uint32_t base = full << wl, r = g->n - base, jr = j - base;
+        h = 31u - (uint32_t)__builtin_clz(r ^ jr);
+        q = full + (uint32_t)__builtin_popcount(r >> (h + 1));
+        off = base + (r & ~((2u << h) - 1));
+    }
+    leaf_tree[i] = t0 + q;
+    if (j == off) trees[t0 + q] = Tree{g->start + off, h};
+    return lo;
+}
+
 // Leaf node of every blob share, hashed straight from the blob bytes (the
 // sparse share is never materialised).  Message = 0x00 || ns || share (542 B,
 // 9 blocks) with share = ns || info || [len BE32 if first] || data || zeros:
@@ -78,11 +121,12 @@ __device__ __forceinline__ uint32_t data_word(uint32_t lo, uint32_t hi, uint32_t
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void blob_leaf_kernel(
-    const square::Segment* __restrict__ segs, const uint32_t* __restrict__ leaf_seg,
-    const uint8_t* __restrict__ data, uint8_t* __restrict__ slots, uint32_t n_leaves) {
+    const square::Segment* __restrict__ segs, uint32_t n_segs, const uint32_t* __restrict__ seg_tree0,
+    Tree* __restrict__ trees, uint32_t* __restrict__ leaf_tree, const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ slots, uint32_t n_leaves) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n_leaves) return;
-    const square::Segment* g = segs + leaf_seg[i];
+    const square::Segment* g = segs + leaf_tables(i, segs, n_segs, seg_tree0, trees, leaf_tree);
     if (g->kind != square::kSegBlob) return;   // alignment gap: never read by a used node
     const uint32_t j = i - g->start, len = g->len;
     const bool first = j == 0;
@@ -175,48 +219,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
     store_slot(slots + (size_t)i * kSlot, out);
 }
 
-// Per-leaf segment and subtree index tables, built on the device from the
-// plan's segment list (binary search per leaf) instead of shipping 8 bytes per
-// leaf over PCIe.  The subtree list is written here too: a blob's subtrees
-// (inclusion.MerkleMountainRangeSizes: n >> sub_log full ones, then one per
-// set bit of the remainder r, largest first) follow from its segment, and the
-// first leaf of each subtree writes its record.  A remainder leaf j lies in
-// the subtree of the highest bit where j and r differ (r has it set).
-__global__ __launch_bounds__(256) void leaf_tables_kernel(const square::Segment* __restrict__ segs, uint32_t n_segs,
-                                                          const uint32_t* __restrict__ seg_tree0,
-                                                          Tree* __restrict__ trees, uint32_t* __restrict__ leaf_seg,
-                                                          uint32_t* __restrict__ leaf_tree, uint32_t n_leaves) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n_leaves) return;
-    uint32_t lo = 0, hi = n_segs;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (segs[mid].start <= i) lo = mid;
-        else hi = mid;
-    }
-    leaf_seg[i] = lo;
-    const uint32_t t0 = seg_tree0[lo];
-    const square::Segment* g = segs + lo;
-    if (t0 == square::kNoTree || g->kind != square::kSegBlob) {
-        leaf_tree[i] = square::kNoTree;
-        return;
-    }
-    const uint32_t j = i - g->start, wl = g->sub_log, full = g->n >> wl;
-    uint32_t q, off, h;
-    if ((j >> wl) < full) {
-        q = j >> wl;
-        off = q << wl;
-        h = wl;
-    } else {
-        const uint32_t base = full << wl, r = g->n - base, jr = j - base;
-        h = 31u - (uint32_t)__builtin_clz(r ^ jr);
-        q = full + (uint32_t)__builtin_popcount(r >> (h + 1));
-        off = base + (r & ~((2u << h) - 1));
-    }
-    leaf_tree[i] = t0 + q;
-    if (j == off) trees[t0 + q] = Tree{g->start + off, h};
-}
-
 // Height-0 subtrees (single share): the root is the leaf node itself.
 __global__ __launch_bounds__(256) void leaf_roots_kernel(const Tree* __restrict__ trees, uint32_t n_trees,
                                                          const uint8_t* __restrict__ leaf_slots,
@@ -234,7 +236,16 @@ __global__ __launch_bounds__(256) void subtree_level_kernel(const Tree* __restri
                                                             uint32_t* __restrict__ dig, uint32_t level,
                                                             uint32_t n_nodes) {
     const uint32_t n = blockIdx.x * 256 + threadIdx.x;
-    if (n >= n_nodes) return;
+    if (n >= n_nodes) {
+        // level 1 also takes the height-0 subtrees (a single share: its RFC
+        // leaf digest is of the leaf node itself), off the launch chain
+        const uint32_t t = n - n_nodes;
+        if (level != 1 || t >= n_trees || trees[t].height != 0) return;
+        uint32_t I[kSlotWords];
+        load_slot_be(in + (size_t)trees[t].off * kSlot, I);
+        store_rfc_leaf(I, dig + (size_t)t * 8);
+        return;
+    }
     const uint32_t leaf0 = n << level;
     const uint32_t lo = leaf_tree[leaf0];   // subtree holding leaf0 (kNoTree: alignment gap)
     if (lo == square::kNoTree) return;
@@ -566,25 +577,24 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
         if ((rc = check(cm_leaf_.ensure((size_t)N * kSlot), "hipMalloc"))) return rc;
         if ((rc = check(cm_lvl_.ensure((size_t)(N / 2 + 1) * kSlot), "hipMalloc"))) return rc;
         if ((rc = check(cm_roots_.ensure((size_t)n_trees * 32), "hipMalloc"))) return rc;   // RFC leaf digests
-        if ((rc = check(cm_tables_.ensure((size_t)N * 8 + (size_t)n_trees * sizeof(Tree)), "hipMalloc"))) return rc;
-        uint32_t* d_leaf_seg = cm_tables_.as<uint32_t>();
-        uint32_t* d_leaf_tree = d_leaf_seg + N;
+        if ((rc = check(cm_tables_.ensure((size_t)N * 4 + (size_t)n_trees * sizeof(Tree)), "hipMalloc"))) return rc;
+        uint32_t* d_leaf_tree = cm_tables_.as<uint32_t>();
         Tree* d_trees = reinterpret_cast<Tree*>(d_leaf_tree + N);
-        hipLaunchKernelGGL(leaf_tables_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, (uint32_t)p.segs.size(),
-                           d_st, d_trees, d_leaf_seg, d_leaf_tree, N);
-        if ((rc = check(hipGetLastError(), "leaf tables"))) return rc;
-        hipLaunchKernelGGL(blob_leaf_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, d_leaf_seg, d_data,
-                           cm_leaf_.as<uint8_t>(), N);
+        hipLaunchKernelGGL(blob_leaf_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, (uint32_t)p.segs.size(),
+                           d_st, d_trees, d_leaf_tree, d_data, cm_leaf_.as<uint8_t>(), N);
         if ((rc = check(hipGetLastError(), "blob leaves"))) return rc;
-        hipLaunchKernelGGL(leaf_roots_kernel, dim3((n_trees + 255) / 256), dim3(256), 0, s, d_trees, n_trees,
-                           cm_leaf_.as<uint8_t>(), cm_roots_.as<uint32_t>());
-        if ((rc = check(hipGetLastError(), "leaf roots"))) return rc;
+        if (p.max_height == 0) {   // else the level-1 launch hashes the height-0 subtrees too
+            hipLaunchKernelGGL(leaf_roots_kernel, dim3((n_trees + 255) / 256), dim3(256), 0, s, d_trees, n_trees,
+                               cm_leaf_.as<uint8_t>(), cm_roots_.as<uint32_t>());
+            if ((rc = check(hipGetLastError(), "leaf roots"))) return rc;
+        }
         for (uint32_t L = 1; L <= p.max_height; L++) {
             uint8_t* in = (L - 1) % 2 == 0 ? cm_leaf_.as<uint8_t>() : cm_lvl_.as<uint8_t>();
             uint8_t* out = L % 2 == 0 ? cm_leaf_.as<uint8_t>() : cm_lvl_.as<uint8_t>();
             const uint32_t n_nodes = (uint32_t)(((uint64_t)N + (1ull << L) - 1) >> L);
-            hipLaunchKernelGGL(subtree_level_kernel, dim3((n_nodes + 255) / 256), dim3(256), 0, s, d_trees, n_trees,
-                               d_leaf_tree, in, out, cm_roots_.as<uint32_t>(), L, n_nodes);
+            const uint64_t threads = (uint64_t)n_nodes + (L == 1 ? n_trees : 0u);
+            hipLaunchKernelGGL(subtree_level_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, d_trees,
+                               n_trees, d_leaf_tree, in, out, cm_roots_.as<uint32_t>(), L, n_nodes);
             if ((rc = check(hipGetLastError(), "subtree level"))) return rc;
         }
     }
