@@ -565,8 +565,9 @@ def eds_repair(ctx, k: int = 128, reps: int = 5) -> dict:
         assert np.array_equal(d.cpu().numpy().reshape(W, W, 512), full), "device-repaired square differs"
         med = lambda t: 1e3 * sorted(t[1:])[len(t[1:]) // 2]  # noqa: E731
         out[name] = {"erased_cells": int((p == 0).sum()), "ms_device": med(dev_t), "ms_host_buffers": med(host_t)}
-    out["note"] = ("ms_device: cda_repair_device on an HBM-resident square (wall, includes the pre-repair "
-                   "root/parity sanity check and the final verification, each a full NMT + re-encode pass); "
+    out["note"] = ("ms_device: cda_repair_device on an HBM-resident square (wall: pristine copy, decode sweeps, "
+                   "and the final verification of every row and column -- a full NMT + re-encode pass, which also "
+                   "covers rsmt2d's pre-repair sanity check; that check runs separately only on the error path); "
                    "ms_host_buffers adds the 32 MiB copies each way")
     return out
 

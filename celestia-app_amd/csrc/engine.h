@@ -302,6 +302,11 @@ class Engine {
     // repair: GF(2^8) tables (GF(2^16) ones are shared with the encoder),
     // codeword list, error locators, presence map, parity check scratch
     DevBuf gf8_log_, gf8_exp_, gf8_skew_, rp_cw_, rp_err_, rp_present_, rp_parity_, rp_buf_, rp_flags_;
+    // pinned staging of repair's small uploads (presence map, codeword lists):
+    // copies stay asynchronous; the cursor restarts after a stream sync
+    void* rp_host_ = nullptr;
+    size_t rp_host_bytes_ = 0, rp_host_used_ = 0;
+    uint8_t* rp_stage(const void* src, size_t n, hipStream_t s, int* rc);
     std::vector<uint8_t> rp_roots_;
     // standalone trees: host cells, all tree levels, axis indexes / error words, roots
     DevBuf tr_cells_, tr_levels_, tr_axis_, tr_roots_;

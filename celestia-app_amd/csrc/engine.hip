@@ -60,6 +60,7 @@ Engine::~Engine() {
         b->release();
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);
+    if (rp_host_) (void)hipHostFree(rp_host_);
     for (Mark& m : marks_) {
         if (m.a) (void)hipEventDestroy(m.a);
         if (m.b) (void)hipEventDestroy(m.b);

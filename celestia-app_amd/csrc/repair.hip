@@ -303,6 +303,30 @@ int Engine::ensure_gf8_tables() {
     return CDA_OK;
 }
 
+// Copies n host bytes into the pinned staging area and returns the staged
+// address (for an async H2D on s).  When the area is full, waits for s
+// (the earlier copies out of it are then done) and starts over.
+uint8_t* Engine::rp_stage(const void* src, size_t n, hipStream_t s, int* rc) {
+    const size_t need = (n + 63) & ~(size_t)63;
+    if (rp_host_used_ + need > rp_host_bytes_) {
+        if ((*rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return nullptr;
+        rp_host_used_ = 0;
+        if (need > rp_host_bytes_) {
+            if (rp_host_) (void)hipHostFree(rp_host_);
+            rp_host_ = nullptr;
+            rp_host_bytes_ = 0;
+            const size_t cap = std::max(need, (size_t)4 << 20);
+            if ((*rc = check(hipHostMalloc(&rp_host_, cap, hipHostMallocDefault), "hipHostMalloc"))) return nullptr;
+            rp_host_bytes_ = cap;
+        }
+    }
+    uint8_t* p = static_cast<uint8_t*>(rp_host_) + rp_host_used_;
+    std::memcpy(p, src, n);
+    rp_host_used_ += need;
+    *rc = CDA_OK;
+    return p;
+}
+
 int Engine::decode_codewords(uint8_t* d_eds, uint8_t* d_present, uint32_t k, uint32_t shard_len,
                              const std::vector<uint32_t>& axis_index, hipStream_t s) {
     const uint32_t n_cw = (uint32_t)axis_index.size() / 2;
@@ -318,8 +342,9 @@ int Engine::decode_codewords(uint8_t* d_eds, uint8_t* d_present, uint32_t k, uin
     }
     if ((rc = check(rp_cw_.ensure((size_t)n_cw * sizeof(Cw)), "hipMalloc"))) return rc;
     if ((rc = check(rp_err_.ensure((size_t)n_cw * n * 2), "hipMalloc"))) return rc;
-    if ((rc = check(hipMemcpyAsync(rp_cw_.ptr, axis_index.data(), (size_t)n_cw * sizeof(Cw), hipMemcpyHostToDevice, s),
-                    "H2D")))
+    const uint8_t* staged = rp_stage(axis_index.data(), (size_t)n_cw * sizeof(Cw), s, &rc);
+    if (!staged) return rc;
+    if ((rc = check(hipMemcpyAsync(rp_cw_.ptr, staged, (size_t)n_cw * sizeof(Cw), hipMemcpyHostToDevice, s), "H2D")))
         return rc;
     hipLaunchKernelGGL(errloc_kernel, dim3(n_cw), dim3(256), n * 4, s, F, rp_cw_.as<Cw>(), d_present, k,
                        rp_err_.as<uint16_t>());
@@ -341,9 +366,7 @@ int Engine::decode_codewords(uint8_t* d_eds, uint8_t* d_present, uint32_t k, uin
     }
     if ((rc = check(hipGetLastError(), "decode"))) return rc;
     hipLaunchKernelGGL(mark_kernel, dim3((n_cw * n + 255) / 256), dim3(256), 0, s, rp_cw_.as<Cw>(), n_cw, d_present, n);
-    if ((rc = check(hipGetLastError(), "mark"))) return rc;
-    // the host vector `axis_index` is pageable: wait for its copy
-    return check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return check(hipGetLastError(), "mark");
 }
 
 namespace {
@@ -416,7 +439,8 @@ int Engine::repair_verify(const uint8_t* E, uint32_t k, const uint8_t* row_roots
 // Fast path: sweeps that decode every decodable row at once, then every
 // decodable column, up to the fixed point of "decode any vector with >= k
 // cells" (unique, so the reference's row/column interleaving reaches the
-// same one), then one verification of every complete vector.  When all of
+// same one), then one verification of every complete vector (which covers
+// the reference's pre-repair sanity check: see precheck).  When all of
 // them match their roots and are codewords, each decode the reference would
 // have run saw cells of that same codeword, so its result and its checks are
 // the ones of the fast path (MDS uniqueness, by induction over its order).
@@ -445,6 +469,9 @@ int Engine::repair(uint8_t* eds, uint8_t* d_eds, const uint8_t* present_in, uint
     const size_t eds_b = (size_t)W * W * kShare, roots_b = (size_t)W * kNode;
     hipStream_t s = stream_;
     int rc;
+    // earlier copies out of the staging area are done once s is idle
+    if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    rp_host_used_ = 0;
     DevBuf& stage = d_eds ? rp_buf_ : h_eds_;
     if ((rc = check(stage.ensure(eds_b), "hipMalloc"))) return rc;
     if ((rc = check(rp_present_.ensure((size_t)W * W), "hipMalloc"))) return rc;
@@ -467,10 +494,9 @@ int Engine::repair(uint8_t* eds, uint8_t* d_eds, const uint8_t* present_in, uint
             return r;
         }
         first = false;
-        if ((r = check(hipMemcpyAsync(rp_present_.ptr, present.data(), present.size(), hipMemcpyHostToDevice, s),
-                       "H2D")))
-            return r;
-        return check(hipStreamSynchronize(s), "hipStreamSynchronize");
+        const uint8_t* staged = rp_stage(present.data(), present.size(), s, &r);
+        if (!staged) return r;
+        return check(hipMemcpyAsync(rp_present_.ptr, staged, present.size(), hipMemcpyHostToDevice, s), "H2D");
     };
     auto cell = [&](uint32_t axis, uint32_t i, uint32_t p) {
         return axis == 0 ? (size_t)i * W + p : (size_t)p * W + i;
@@ -496,26 +522,32 @@ int Engine::repair(uint8_t* eds, uint8_t* d_eds, const uint8_t* present_in, uint
         return r == code ? code : r;
     };
     std::vector<uint8_t> bad;
-    if ((rc = upload())) return rc;
     // ---- preRepairSanityCheck: every complete vector must match its root
     // ("bad root input", a plain error) and re-encode to its parity
     // (ErrByzantineData).  rsmt2d runs these checks in parallel goroutines;
     // the first failure in (index, row before column, root before parity)
-    // order is reported here.
-    if ((rc = repair_verify(E, k, row_roots, col_roots, bad, s))) return rc;
-    for (uint32_t i = 0; i < W; i++)
-        for (uint32_t axis = 0; axis < 2; axis++) {
-            if (count(axis, i) != W) continue;
-            const uint8_t b = bad[axis * W + i];
-            if (b & 1) {
-                char head[64];
-                snprintf(head, sizeof head, "bad root input: %s %u expected ", axis == 0 ? "row" : "col", i);
-                const uint8_t* want = (axis == 0 ? row_roots : col_roots) + (size_t)i * kNode;
-                return fail(CDA_ERR_INVALID, std::string(head) + hex(want, kNode) + " got " +
-                                                 hex(rp_roots_.data() + ((size_t)axis * W + i) * kNode, kNode));
+    // order is reported here.  Run only on the error path: a vector complete
+    // in the input keeps its cells through the sweeps, so a clean final
+    // verification implies this check passed.
+    auto precheck = [&]() -> int {
+        int r;
+        if ((r = repair_verify(E, k, row_roots, col_roots, bad, s))) return r;
+        for (uint32_t i = 0; i < W; i++)
+            for (uint32_t axis = 0; axis < 2; axis++) {
+                if (count(axis, i) != W) continue;
+                const uint8_t b = bad[axis * W + i];
+                if (b & 1) {
+                    char head[64];
+                    snprintf(head, sizeof head, "bad root input: %s %u expected ", axis == 0 ? "row" : "col", i);
+                    const uint8_t* want = (axis == 0 ? row_roots : col_roots) + (size_t)i * kNode;
+                    return fail(CDA_ERR_INVALID, std::string(head) + hex(want, kNode) + " got " +
+                                                     hex(rp_roots_.data() + ((size_t)axis * W + i) * kNode, kNode));
+                }
+                if (b & 2) return byzantine(axis, i);
             }
-            if (b & 2) return byzantine(axis, i);
-        }
+        return CDA_OK;
+    };
+    if ((rc = upload())) return rc;
     // ---- fast path: batched sweeps to the fixed point, then verification
     bool solved = false;
     for (;;) {
@@ -546,8 +578,10 @@ int Engine::repair(uint8_t* eds, uint8_t* d_eds, const uint8_t* present_in, uint
         const int r = download(code);
         return r == code ? code : r;
     }
-    // ---- exact replay of solveCrossword (error path)
+    // ---- error path: from the input again, the sanity check, then the exact
+    // replay of solveCrossword
     if ((rc = upload())) return rc;
+    if ((rc = precheck())) return rc;
     for (;;) {
         bool all = true, progress = false;
         for (uint32_t i = 0; i < W; i++)
@@ -606,6 +640,8 @@ int Engine::host_rs_decode(uint8_t* shards, const uint8_t* present, uint32_t k, 
     hipStream_t s = stream_;
     const size_t b = (size_t)n_codewords * W * shard_len;
     int rc;
+    if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    rp_host_used_ = 0;
     if ((rc = check(rp_buf_.ensure(b), "hipMalloc"))) return rc;
     if ((rc = check(rp_present_.ensure((size_t)n_codewords * W), "hipMalloc"))) return rc;
     if ((rc = check(hipMemcpyAsync(rp_buf_.ptr, shards, b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
