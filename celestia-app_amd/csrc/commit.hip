@@ -349,32 +349,19 @@ __global__ __launch_bounds__(64) void commitment_kernel(const uint32_t* __restri
     }
 }
 
-// Blob groups: one wave takes the consecutive blobs [group_blob0[g],
-// group_blob0[g + 1]) (at most 64) and runs their RFC-6962 levels together:
-// each level's parents of all the group's blobs are one flat list of units
-// over the wave's lanes (a lane pair per unit when they fit, else a lane per
-// unit), so the narrow upper levels of one blob share the wave's instruction
-// stream with those of its neighbours instead of idling 60 of 64 lanes.  The
-// digests stay in LDS, each blob's level compacted in place at the front of
-// its own slot range (every unit reads its two children before any unit
-// writes; the odd node is promoted after the level's writes).
-__global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __restrict__ dig,
-                                                               const uint32_t* __restrict__ blob_tree0,
-                                                               const uint32_t* __restrict__ group_blob0,
-                                                               uint8_t* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [group trees][8]
-    __shared__ uint32_t pre[64], bbase[64];
-    const uint32_t b0 = group_blob0[blockIdx.x], G = group_blob0[blockIdx.x + 1] - b0;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t t_base = blob_tree0[b0], T = blob_tree0[b0 + G] - t_base;
-    for (uint32_t i = lane; i < T * 8; i += 64) hs[i] = dig[(size_t)t_base * 8 + i];
-    uint32_t m = 0, base = 0;
-    if (lane < G) {
-        base = blob_tree0[b0 + lane] - t_base;
-        m = blob_tree0[b0 + lane + 1] - blob_tree0[b0 + lane];
-        bbase[lane] = base;
-    }
-    __syncthreads();
+// RFC-6962 levels of a group of G <= 64 consecutive blobs whose subtree-root
+// digests sit in LDS (hs, blob i's at slots [bbase[i], bbase[i] + m_i)), by
+// NT threads: each level's parents of all the group's blobs are one flat
+// unit list (a lane pair per unit when they fit, else a lane per unit in
+// passes), compacted in place at the front of each blob's slot range (every
+// unit reads its two children before any unit writes; the odd node is
+// promoted after the level's writes).  Wave 0's lanes i < G hold m_i / base_i
+// and write blob i's commitment.
+template <int NT>
+__device__ __forceinline__ void group_rfc_levels(uint32_t* hs, uint32_t G, uint32_t m, uint32_t base, uint32_t b0,
+                                                 uint32_t* pre, const uint32_t* bbase, uint32_t* s_total,
+                                                 uint8_t* __restrict__ out, bool pair_ok) {
+    const uint32_t tid = threadIdx.x;
     // blob of unit u: the first i with pre[i] > u (pre = inclusive prefix of
     // the level's parent counts)
     auto find = [&](uint32_t u) {
@@ -389,15 +376,16 @@ __global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __
     };
     for (;;) {
         const uint32_t p = m / 2;
-        uint32_t sc = p;
+        if (tid < 64) {
+            uint32_t sc = p;
 #pragma unroll
-        for (int k = 1; k < 64; k <<= 1) {
-            const uint32_t v = __shfl_up(sc, k, 64);
-            if (lane >= (uint32_t)k) sc += v;
+            for (int k = 1; k < 64; k <<= 1) {
+                const uint32_t v = __shfl_up(sc, k, 64);
+                if (tid >= (uint32_t)k) sc += v;
+            }
+            pre[tid] = sc;
+            if (tid == 63) *s_total = sc;
         }
-        const uint32_t total = __shfl(sc, 63, 64);
-        if (total == 0) break;
-        pre[lane] = sc;
         const bool odd = (m & 1) && m > 1;
         uint32_t carry[8];
         if (odd) {
@@ -405,9 +393,11 @@ __global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __
             for (int j = 0; j < 8; j++) carry[j] = hs[(base + m - 1) * 8 + j];
         }
         __syncthreads();
-        if (2 * total <= 64) {
-            const uint32_t u = lane >> 1;
-            const bool A = lane & 1;
+        const uint32_t total = *s_total;
+        if (total == 0) break;
+        if (pair_ok && 2 * total <= NT) {
+            const uint32_t u = tid >> 1;
+            const bool A = tid & 1;
             uint32_t D[8], slot = 0;
             if (u < total) {
                 const uint32_t i = find(u);
@@ -429,8 +419,8 @@ __global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __
             }
         } else {
             // a later pass's children lie past every slot an earlier pass wrote
-            for (uint32_t u0 = 0; u0 < total; u0 += 64) {
-                const uint32_t u = u0 + lane;
+            for (uint32_t u0 = 0; u0 < total; u0 += NT) {
+                const uint32_t u = u0 + tid;
                 uint32_t D[8], slot = 0;
                 if (u < total) {
                     const uint32_t i = find(u);
@@ -454,8 +444,8 @@ __global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __
         m = p + (m & 1);
         __syncthreads();
     }
-    if (lane < G) {
-        uint32_t* o = reinterpret_cast<uint32_t*>(out + (size_t)(b0 + lane) * 32);
+    if (tid < G) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + (size_t)(b0 + tid) * 32);
         if (m == 0) {   // no shares: merkle.HashFromByteSlices(nil) = sha256("")
             const uint32_t e[8] = {0x42c4b0e3u, 0x141cfc98u, 0xc8f4fb9au, 0x24b96f99u,
                                    0xe441ae27u, 0x4c939b64u, 0x1b9995a4u, 0x55b85278u};
@@ -466,6 +456,137 @@ __global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __
             for (int j = 0; j < 8; j++) o[j] = bswap32(hs[base * 8 + j]);
         }
     }
+}
+
+// Blob groups: one wave takes the consecutive blobs [group_blob0[g],
+// group_blob0[g + 1]) (at most 64) and runs their RFC-6962 levels together
+// (group_rfc_levels), so the narrow upper levels of one blob share the
+// wave's instruction stream with those of its neighbours instead of idling
+// 60 of 64 lanes.
+__global__ __launch_bounds__(64) void commitment_group_kernel(const uint32_t* __restrict__ dig,
+                                                               const uint32_t* __restrict__ blob_tree0,
+                                                               const uint32_t* __restrict__ group_blob0,
+                                                               uint8_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [group trees][8]
+    __shared__ uint32_t pre[64], bbase[64], s_total;
+    const uint32_t b0 = group_blob0[blockIdx.x], G = group_blob0[blockIdx.x + 1] - b0;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t t_base = blob_tree0[b0], T = blob_tree0[b0 + G] - t_base;
+    for (uint32_t i = lane; i < T * 8; i += 64) hs[i] = dig[(size_t)t_base * 8 + i];
+    uint32_t m = 0, base = 0;
+    if (lane < G) {
+        base = blob_tree0[b0 + lane] - t_base;
+        m = blob_tree0[b0 + lane + 1] - blob_tree0[b0 + lane];
+        bbase[lane] = base;
+    }
+    __syncthreads();
+    group_rfc_levels<64>(hs, G, m, base, b0, pre, bbase, &s_total, out, true);
+}
+
+// Small batches of small blobs (every blob at most kFusedMaxShares shares,
+// at most one group per CU -- the latency case, e.g. one block's blobs in
+// ProcessProposal): one 256-thread workgroup per group of consecutive blobs
+// also runs the subtree
+// levels, in LDS, after blob_leaf_kernel -- no launch per level, no slot
+// round trips through HBM.  The group's leaf slots are loaded once
+// (big-endian words); node n of level L lives at the slot of its first leaf
+// (n << L), so a parent overwrites only its own left child and a level
+// needs no barrier between reads and writes.  Subtree roots go straight to
+// their RFC-6962 leaf digests, then group_rfc_levels.
+constexpr uint32_t kFusedMaxShares = 512;
+__global__ __launch_bounds__(256) void commitment_fused_kernel(const uint8_t* __restrict__ leaf_slots,
+                                                               const Tree* __restrict__ trees,
+                                                               const uint32_t* __restrict__ leaf_tree,
+                                                               const uint32_t* __restrict__ blob_tree0,
+                                                               const uint32_t* __restrict__ group_blob0,
+                                                               uint8_t* __restrict__ out, uint32_t pair_ok) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    __shared__ uint32_t pre[64], bbase[64], s_total, s_maxh;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b0 = group_blob0[blockIdx.x], G = group_blob0[blockIdx.x + 1] - b0;
+    const uint32_t T0 = blob_tree0[b0], T = blob_tree0[b0 + G] - T0;
+    uint32_t L0 = 0, NL = 0;
+    if (T) {
+        const Tree first = trees[T0], last = trees[T0 + T - 1];
+        L0 = first.off;
+        NL = last.off + (1u << last.height) - L0;
+    }
+    uint32_t* slots = sm;                     // [NL][24] big-endian words
+    uint32_t* dig = sm + NL * kSlotWords;     // [T][8] subtree roots' RFC leaf digests
+    for (uint32_t i = tid; i < NL * 6; i += 256) {
+        const uint4 v = *reinterpret_cast<const uint4*>(leaf_slots + (size_t)(L0 + i / 6) * kSlot + (i % 6) * 16);
+        uint32_t* d = slots + (i / 6) * kSlotWords + (i % 6) * 4;
+        d[0] = bswap32(v.x);
+        d[1] = bswap32(v.y);
+        d[2] = bswap32(v.z);
+        d[3] = bswap32(v.w);
+    }
+    if (tid == 0) s_maxh = 0;
+    __syncthreads();
+    for (uint32_t t = tid; t < T; t += 256) {
+        const Tree tr = trees[T0 + t];
+        atomicMax(&s_maxh, tr.height);
+        if (tr.height == 0) {   // a single share: the leaf is the subtree root
+            uint32_t I[kSlotWords], D[8];
+#pragma unroll
+            for (int j = 0; j < kSlotWords; j++) I[j] = slots[(tr.off - L0) * kSlotWords + j];
+            rfc_leaf_u<false>(I, D, false);
+#pragma unroll
+            for (int j = 0; j < 8; j++) dig[t * 8 + j] = D[j];
+        }
+    }
+    __syncthreads();
+    const uint32_t maxh = s_maxh;
+    for (uint32_t L = 1; L <= maxh; L++) {
+        const uint32_t n_lo = L0 >> L, cnt = ((L0 + NL - 1) >> L) - n_lo + 1;
+        auto node = [&](uint32_t n, bool pair, bool A) {
+            const uint32_t leaf0 = n << L;
+            if (leaf0 < L0) return;
+            const uint32_t lo = leaf_tree[leaf0];
+            if (lo == square::kNoTree) return;
+            const uint32_t h = trees[lo].height;
+            if (h < L) return;
+            uint32_t Lw[kSlotWords], Rw[kSlotWords], o[kSlotWords];
+            const uint32_t* pl = slots + (leaf0 - L0) * kSlotWords;
+            const uint32_t* pr = slots + (leaf0 + (1u << (L - 1)) - L0) * kSlotWords;
+#pragma unroll
+            for (int j = 0; j < kSlotWords; j++) {
+                Lw[j] = pl[j];
+                Rw[j] = pr[j];
+            }
+            if (pair) hash_node_u<true>(Lw, Rw, o, A);
+            else hash_node_u<false>(Lw, Rw, o, false);
+#pragma unroll
+            for (int j = 0; j < kSlotWords; j++) o[j] = bswap32(o[j]);   // big-endian view
+            if (h == L) {   // subtree root -> its RFC-6962 leaf digest
+                uint32_t D[8];
+                if (pair) rfc_leaf_u<true>(o, D, A);
+                else rfc_leaf_u<false>(o, D, false);
+                if (!A) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) dig[(lo - T0) * 8 + j] = D[j];
+                }
+            } else if (!A) {
+                uint32_t* po = slots + (leaf0 - L0) * kSlotWords;
+#pragma unroll
+                for (int j = 0; j < kSlotWords; j++) po[j] = o[j];
+            }
+        };
+        if (pair_ok && 2 * cnt <= 256) {
+            if ((tid >> 1) < cnt) node(n_lo + (tid >> 1), true, tid & 1);
+        } else {
+            for (uint32_t i = tid; i < cnt; i += 256) node(n_lo + i, false, false);
+        }
+        __syncthreads();
+    }
+    uint32_t m = 0, base = 0;
+    if (tid < G) {
+        base = blob_tree0[b0 + tid] - T0;
+        m = blob_tree0[b0 + tid + 1] - blob_tree0[b0 + tid];
+        bbase[tid] = base;
+    }
+    __syncthreads();
+    group_rfc_levels<256>(dig, G, m, base, b0, pre, bbase, &s_total, out, pair_ok != 0);
 }
 
 // RFC-6962 leaf digests of n 96-B slots.
@@ -507,6 +628,12 @@ static bool group_commitments() {
     }();
     return on;
 }
+// CDA_COMMIT_FUSED=0: small-blob batches also take the level launches and
+// commitment_group_kernel instead of commitment_fused_kernel (read per call).
+static bool fuse_commitments() {
+    const char* e = std::getenv("CDA_COMMIT_FUSED");
+    return !(e && e[0] == '0');
+}
 
 int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, const uint8_t* d_data, uint8_t* d_out,
                                 hipStream_t s) {
@@ -521,7 +648,55 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
     std::vector<uint32_t>& grp = cm_groups_;
     grp.clear();
     uint32_t max_gt = 0;
-    if (group_commitments()) {
+    // Small-blob batches take commitment_fused_kernel (subtree levels in LDS
+    // too): groups of consecutive blobs whose leaf range (alignment gaps
+    // included) stays within kFusedGroupLeaves -- a single blob up to
+    // kFusedMaxShares -- sized for three workgroups per CU.
+    constexpr uint32_t kFusedGroupLeaves = 384, kFusedMaxGroups = 256;
+    uint32_t max_sh = 0;
+    for (const auto& g : p.segs)
+        if (g.kind == square::kSegBlob) max_sh = std::max(max_sh, g.n);
+    bool fused = group_commitments() && fuse_commitments() && p.n_leaves && max_sh <= kFusedMaxShares;
+    size_t fused_lds = 0;
+    if (fused) {
+        const uint32_t* bt = p.blob_tree0.data();
+        size_t si = 0;
+        uint32_t g0 = 0, gl0 = 0, gl1 = 0, gt = 0;
+        auto close = [&]() {
+            fused_lds = std::max(fused_lds, ((size_t)(gl1 - gl0) * kSlotWords + (size_t)gt * 8) * 4);
+        };
+        grp.push_back(0);
+        for (uint32_t b = 0; b < n_blobs; b++) {
+            const uint32_t nt = bt[b + 1] - bt[b];
+            uint32_t s0 = 0, s1 = 0;
+            if (nt) {   // the blob's segment: blobs with shares have one each, in order
+                while (p.segs[si].kind != square::kSegBlob) si++;
+                s0 = p.segs[si].start;
+                s1 = s0 + p.segs[si].n;
+                si++;
+            }
+            if (b > g0 && (b - g0 == 64 || (nt && gt && s1 - gl0 > kFusedGroupLeaves))) {
+                close();
+                grp.push_back(b);
+                g0 = b;
+                gl0 = gl1 = gt = 0;
+            }
+            if (nt) {
+                if (!gt) gl0 = s0;
+                gl1 = s1;
+                gt += nt;
+            }
+        }
+        grp.push_back(n_blobs);
+        close();
+        // a latency path: with more groups than CUs the level launches pack
+        // the chip better (64 full blocks: 0.49 ms unfused, 0.67 fused)
+        if (grp.size() - 1 > kFusedMaxGroups) {
+            fused = false;
+            grp.clear();
+        }
+    }
+    if (!fused && group_commitments()) {
         const uint32_t* bt = p.blob_tree0.data();
         uint64_t units = 0;
         for (uint32_t b = 0; b < n_blobs; b++) units += (bt[b + 1] - bt[b]) / 2;
@@ -583,6 +758,19 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
         hipLaunchKernelGGL(blob_leaf_kernel, dim3((N + 255) / 256), dim3(256), 0, s, d_segs, (uint32_t)p.segs.size(),
                            d_st, d_trees, d_leaf_tree, d_data, cm_leaf_.as<uint8_t>(), N);
         if ((rc = check(hipGetLastError(), "blob leaves"))) return rc;
+        if (fused) {
+            if (fused_lds > 48 * 1024 &&
+                (rc = check(hipFuncSetAttribute(reinterpret_cast<const void*>(commitment_fused_kernel),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fused_lds),
+                            "hipFuncSetAttribute")))
+                return rc;
+            // lane pairs cut a compression's latency but cost 1.6x its lane
+            // work: kept for when the groups leave most of the chip idle
+            const uint32_t n_groups = (uint32_t)grp.size() - 1, pair_ok = n_groups <= 512 ? 1u : 0u;
+            hipLaunchKernelGGL(commitment_fused_kernel, dim3(n_groups), dim3(256), fused_lds, s, cm_leaf_.as<uint8_t>(),
+                               d_trees, d_leaf_tree, d_bt, d_grp, d_out, pair_ok);
+            return check(hipGetLastError(), "commitments");
+        }
         if (p.max_height == 0) {   // else the level-1 launch hashes the height-0 subtrees too
             hipLaunchKernelGGL(leaf_roots_kernel, dim3((n_trees + 255) / 256), dim3(256), 0, s, d_trees, n_trees,
                                cm_leaf_.as<uint8_t>(), cm_roots_.as<uint32_t>());

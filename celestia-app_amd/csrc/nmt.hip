@@ -306,22 +306,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
     }
 }
 
-// HashNode (no mid-state branch: the tails mix data- and parity-left parents).
-template <bool PAIR>
-__device__ __forceinline__ void hash_node_u(const uint32_t (&L)[kSlotWords], const uint32_t (&R)[kSlotWords],
-                                            uint32_t (&o)[kSlotWords], bool A) {
-    Sha<PAIR> h;
-    h.init(A);
-    uint32_t w[16], D[8];
-#pragma unroll
-    for (int b = 0; b < 3; b++) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
-        h.compress(w, A);
-    }
-    h.digest(A, D);
-    inner_node_words(L, R, D, o);
-}
 // ---------------------------------------------------------------------------
 // Fused top of the trees (latency-bound part: fewer parents than the chip has
 // wave slots).  One workgroup takes tpw trees and runs every remaining level

@@ -432,4 +432,23 @@ CDA_HD void rfc_inner_u(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t
     h.digest(A, D);
 }
 
+// NMT HashNode of two child slots (big-endian words) into a parent slot
+// (little-endian words), per thread or per lane pair; no mid-state branch
+// (the tails mix data- and parity-left parents).
+template <bool PAIR>
+CDA_HD void hash_node_u(const uint32_t (&L)[kSlotWords], const uint32_t (&R)[kSlotWords],
+                                            uint32_t (&o)[kSlotWords], bool A) {
+    Sha<PAIR> h;
+    h.init(A);
+    uint32_t w[16], D[8];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * b + i);
+        h.compress(w, A);
+    }
+    h.digest(A, D);
+    inner_node_words(L, R, D, o);
+}
+
 }  // namespace cda

@@ -95,17 +95,35 @@ def test_commitments_batch_many_small_gpu(ctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ucap", ["1", "100", "1000"])
-def test_commitments_blob_groups_gpu(ctx, ucap, monkeypatch):
+@pytest.mark.parametrize("ucap,fused", [("1", "0"), ("100", "0"), ("1000", "0"), ("32", "1")])
+def test_commitments_blob_groups_gpu(ctx, ucap, fused, monkeypatch):
     """commit.hip commitment_group_kernel with forced group sizes: one blob per
     wave (ucap 1), groups whose levels take lane pairs and single lanes, and
     groups of up to 64 blobs whose first levels take several passes of the
-    wave (ucap 1000), including empty and one-share blobs."""
+    wave (ucap 1000), including empty and one-share blobs; and the same
+    batch through commitment_fused_kernel (subtree levels in LDS, the
+    default for blobs of at most 512 shares)."""
     monkeypatch.setenv("CDA_COMMIT_UCAP", ucap)
+    monkeypatch.setenv("CDA_COMMIT_FUSED", fused)
     rng = np.random.default_rng(21)
     sizes = [int(x) for x in rng.integers(1, 60_000, 150)] + [0, 1, 478, 0] + [int(x) for x in rng.integers(1, 900, 40)]
     blobs = random_blobs(21, sizes)
     for threshold in (64, 2):
+        got = ginc.create_commitments(blobs, threshold)
+        for b, c in zip(blobs, got):
+            assert c == oinc.create_commitment(b.namespace, b.data, 0, threshold), (len(b.data), threshold)
+
+
+@pytest.mark.gpu
+def test_commitments_fused_edges_gpu(ctx):
+    """commitment_fused_kernel at its limits: 512-share blobs alone in their
+    group, groups up to the 384-leaf cap with alignment gaps, 64 tiny blobs
+    in one group, height-0 subtrees (remainder shares), empty blobs."""
+    first, cont = 478, 482
+    sizes = [first + cont * 511, first + cont * 510 + 1, 0, first + cont * 200, 1, 2, first + cont * 7,
+             first + cont * 2 + 5] + [1] * 70 + [first + cont * 63 + 1, 0, first + cont * 130]
+    blobs = random_blobs(23, sizes)
+    for threshold in (64, 8):
         got = ginc.create_commitments(blobs, threshold)
         for b, c in zip(blobs, got):
             assert c == oinc.create_commitment(b.namespace, b.data, 0, threshold), (len(b.data), threshold)
