@@ -37,6 +37,10 @@
 
 #include "cda_kernels.h"
 
+#ifndef CDA_RS16_PROBE
+#define CDA_RS16_PROBE 0
+#endif
+
 namespace cda {
 
 namespace {
@@ -386,10 +390,10 @@ constexpr uint32_t cw_lds_bytes() {
 // =2 drops the global loads and stores (compute + exchanges alone),
 // =3 gives every wave wave 0's pass-A / A' constants (scalar-cache hits),
 // =4 stores one dword per lane and parity shard (half the stores),
-// =5 stores no parity (loads kept).
-#ifndef CDA_RS16_PROBE
-#define CDA_RS16_PROBE 0
-#endif
+// =5 stores no parity (loads kept), =6 drops the exchanges' barriers
+// (timing only, wrong output).  (Dropping the per-group lgkmcnt wait is not a
+// valid probe: an s_load still in flight lands in SGPRs the compiler has
+// reused -- tried once, it faulted.)
 constexpr bool kRs16Compute = CDA_RS16_PROBE != 1, kRs16Memory = CDA_RS16_PROBE != 2;
 
 }  // namespace
@@ -492,16 +496,20 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     // they become residue R*jj + q's shard t -- in place, so pass B's
     // residue q lives in registers {R*t + q}.
     uint32_t lo[S], hi[S];
+    // exchange barrier (CDA_RS16_PROBE == 6: none -- timing probe only)
+    auto xbar = [] {
+        if constexpr (CDA_RS16_PROBE != 6) __syncthreads();
+    };
     auto xchg_a_to_b = [&]() {
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
-            if (q) __syncthreads();
+            if (q) xbar();
             sfor<0, 16, 1>([&](auto jj) {
                 constexpr int j = R * decltype(jj)::value + q;
                 X[((wave * 16 + jj.value) * 2 + 0) * 64 + lane] = lo[j];
                 X[((wave * 16 + jj.value) * 2 + 1) * 64 + lane] = hi[j];
             });
-            __syncthreads();
+            xbar();
             sfor<0, 16, 1>([&](auto tt) {
                 constexpr int j = R * decltype(tt)::value + q;
                 lo[j] = X[((tt.value * 16 + wave) * 2 + 0) * 64 + lane];
@@ -512,13 +520,13 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     auto xchg_b_to_a = [&]() {
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
-            __syncthreads();
+            xbar();
             sfor<0, 16, 1>([&](auto tt) {
                 constexpr int j = R * decltype(tt)::value + q;
                 X[((tt.value * 16 + wave) * 2 + 0) * 64 + lane] = lo[j];
                 X[((tt.value * 16 + wave) * 2 + 1) * 64 + lane] = hi[j];
             });
-            __syncthreads();
+            xbar();
             sfor<0, 16, 1>([&](auto jj) {
                 constexpr int j = R * decltype(jj)::value + q;
                 lo[j] = X[((wave * 16 + jj.value) * 2 + 0) * 64 + lane];
