@@ -306,6 +306,8 @@ class Engine {
     // copies stay asynchronous; the cursor restarts after a stream sync
     void* rp_host_ = nullptr;
     size_t rp_host_bytes_ = 0, rp_host_used_ = 0;
+    void* rp_out_ = nullptr;   // pinned landing area of repair_verify's results
+    size_t rp_out_bytes_ = 0;
     uint8_t* rp_stage(const void* src, size_t n, hipStream_t s, int* rc);
     std::vector<uint8_t> rp_roots_;
     // standalone trees: host cells, all tree levels, axis indexes / error words, roots

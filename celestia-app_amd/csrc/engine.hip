@@ -61,6 +61,7 @@ Engine::~Engine() {
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);
     if (rp_host_) (void)hipHostFree(rp_host_);
+    if (rp_out_) (void)hipHostFree(rp_out_);
     for (Mark& m : marks_) {
         if (m.a) (void)hipEventDestroy(m.a);
         if (m.b) (void)hipEventDestroy(m.b);

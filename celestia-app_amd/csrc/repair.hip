@@ -410,13 +410,26 @@ int Engine::repair_verify(const uint8_t* E, uint32_t k, const uint8_t* row_roots
     hipLaunchKernelGGL(parity_compare_kernel, dim3(2 * W, k), dim3(64), 0, s, E, rp_parity_.as<uint8_t>(), k,
                        rp_flags_.as<uint32_t>());
     if ((rc = check(hipGetLastError(), "parity compare"))) return rc;
-    std::vector<uint8_t> rows(roots_b), cols(roots_b);
-    std::vector<uint32_t> flags(2 * W);
-    if ((rc = check(hipMemcpyAsync(rows.data(), h_rows_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
-    if ((rc = check(hipMemcpyAsync(cols.data(), h_cols_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
-    if ((rc = check(hipMemcpyAsync(flags.data(), rp_flags_.ptr, flags.size() * 4, hipMemcpyDeviceToHost, s), "D2H")))
+    // results land in pinned memory: the copies queue right behind the
+    // kernels (a pageable destination makes each copy wait for the stream and
+    // go through a staging blit)
+    const size_t flags_b = (size_t)2 * W * 4, out_b = 2 * roots_b + flags_b;
+    if (out_b > rp_out_bytes_) {
+        if (rp_out_) (void)hipHostFree(rp_out_);
+        rp_out_ = nullptr;
+        rp_out_bytes_ = 0;
+        if ((rc = check(hipHostMalloc(&rp_out_, out_b, hipHostMallocDefault), "hipHostMalloc"))) return rc;
+        rp_out_bytes_ = out_b;
+    }
+    uint8_t* ob = static_cast<uint8_t*>(rp_out_);
+    if ((rc = check(hipMemcpyAsync(ob, h_rows_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(ob + roots_b, h_cols_.ptr, roots_b, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(ob + 2 * roots_b, rp_flags_.ptr, flags_b, hipMemcpyDeviceToHost, s), "D2H")))
         return rc;
     if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    const std::vector<uint8_t> rows(ob, ob + roots_b), cols(ob + roots_b, ob + 2 * roots_b);
+    std::vector<uint32_t> flags(2 * W);
+    std::memcpy(flags.data(), ob + 2 * roots_b, flags_b);
     bad.assign(2 * W, 0);
     for (uint32_t axis = 0; axis < 2; axis++) {
         const uint8_t* want = axis == 0 ? row_roots : col_roots;
