@@ -48,6 +48,8 @@ __device__ __forceinline__ void lane_rounds(ShaState& s, const uint32_t (&KW)[64
     s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
 
+__constant__ const uint32_t kK[64] = CDA_SHA_K;
+
 template <int V>
 __global__ __launch_bounds__(64) void probe(uint32_t* out, uint64_t* clk, uint32_t seed, int n) {
     const bool A = threadIdx.x & 1;
@@ -75,6 +77,21 @@ __global__ __launch_bounds__(64) void probe(uint32_t* out, uint64_t* clk, uint32
         } else if constexpr (V == 1) {   // lane pair, schedule precomputed
             pair_rounds(ps, KW, A);
             KW[0] ^= ps.h[0];   // keep the chain dependent
+        } else if constexpr (V == 4) {   // one lane, the schedule as its own phase on the same wave
+            uint32_t kw[64];
+#pragma unroll
+            for (int t = 0; t < 16; t++) kw[t] = w[t] + kK[t];
+#pragma unroll
+            for (int t = 16; t < 64; t++) {
+                const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+                w[t & 15] = add3(w[t & 15], xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3), w[(t - 7) & 15]) +
+                            xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                kw[t] = w[t & 15] + kK[t];
+            }
+            asm volatile("" ::: "memory");
+            lane_rounds(ss, kw);
+#pragma unroll
+            for (int j = 0; j < 8; j++) w[j] ^= ss.h[j];
         } else if constexpr (V == 3) {   // one lane, schedule precomputed
             lane_rounds(ss, KW);
             KW[0] ^= ss.h[0];
@@ -113,6 +130,7 @@ int main() {
         run<1>("lane pair, schedule precomputed (K+W)", d, c, p.multiProcessorCount);
         run<2>("one lane per compression", d, c, p.multiProcessorCount);
         run<3>("one lane, schedule precomputed (K+W)", d, c, p.multiProcessorCount);
+        run<4>("one lane, schedule as a separate phase", d, c, p.multiProcessorCount);
     }
     return 0;
 }
