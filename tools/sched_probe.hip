@@ -50,6 +50,44 @@ __device__ __forceinline__ void lane_rounds(ShaState& s, const uint32_t (&KW)[64
 
 __constant__ const uint32_t kK[64] = CDA_SHA_K;
 
+#define SB __builtin_amdgcn_sched_barrier(0);
+// one lane, the schedule word t+16 interleaved op by op into round t, the
+// order pinned with sched_barrier (the scheduler may not move anything
+// across): the schedule's independent ops fill the round chain's stalls
+__device__ __forceinline__ void lane_interleaved(ShaState& s, uint32_t (&w)[16]) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+    uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+    uint32_t kw[64];
+#pragma unroll
+    for (int t = 0; t < 16; t++) kw[t] = w[t] + K[t];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        const bool sc = i + 16 < 64;
+        const int t = i + 16;
+        uint32_t w15 = 0, w2 = 0, r7 = 0, r18 = 0, r17 = 0, r19 = 0, x0 = 0, x1 = 0;
+        uint32_t e6 = rotr(e, 6); SB
+        if (sc) { w15 = w[(t - 15) & 15]; w2 = w[(t - 2) & 15]; r7 = rotr(w15, 7); } SB
+        uint32_t e11 = rotr(e, 11); SB
+        if (sc) r18 = rotr(w15, 18); SB
+        uint32_t e25 = rotr(e, 25); SB
+        if (sc) r17 = rotr(w2, 17); SB
+        const uint32_t S1 = xor3(e6, e11, e25); SB
+        if (sc) r19 = rotr(w2, 19); SB
+        const uint32_t chv = ch(e, f, g); SB
+        if (sc) x0 = xor3(r7, r18, w15 >> 3); SB
+        const uint32_t t1 = add3(h, S1, chv) + kw[i]; SB
+        if (sc) x1 = xor3(r17, r19, w2 >> 10); SB
+        const uint32_t a2 = rotr(a, 2), a13 = rotr(a, 13), a22 = rotr(a, 22); SB
+        if (sc) { w[t & 15] = add3(w[t & 15], x0, w[(t - 7) & 15]) + x1; kw[t] = w[t & 15] + K[t]; } SB
+        const uint32_t S0 = xor3(a2, a13, a22), mj = maj(a, b, c); SB
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = add3(t1, S0, mj);
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
 template <int V>
 __global__ __launch_bounds__(64) void probe(uint32_t* out, uint64_t* clk, uint32_t seed, int n) {
     const bool A = threadIdx.x & 1;
@@ -92,6 +130,10 @@ __global__ __launch_bounds__(64) void probe(uint32_t* out, uint64_t* clk, uint32
             lane_rounds(ss, kw);
 #pragma unroll
             for (int j = 0; j < 8; j++) w[j] ^= ss.h[j];
+        } else if constexpr (V == 5) {   // one lane, hand-interleaved schedule
+            lane_interleaved(ss, w);
+#pragma unroll
+            for (int j = 0; j < 8; j++) w[j] ^= ss.h[j];
         } else if constexpr (V == 3) {   // one lane, schedule precomputed
             lane_rounds(ss, KW);
             KW[0] ^= ss.h[0];
@@ -131,6 +173,7 @@ int main() {
         run<2>("one lane per compression", d, c, p.multiProcessorCount);
         run<3>("one lane, schedule precomputed (K+W)", d, c, p.multiProcessorCount);
         run<4>("one lane, schedule as a separate phase", d, c, p.multiProcessorCount);
+        run<5>("one lane, schedule hand-interleaved", d, c, p.multiProcessorCount);
     }
     return 0;
 }
