@@ -43,6 +43,7 @@ CONFIG5_TIMEOUT_S = float(os.environ.get("CDA_CONFIG5_TIMEOUT_S", "180"))
 ACHIEVABLE_VALU_TOPS = ACHIEVABLE_SHA_COMP_S * SHA_SLOTS / 1e12
 ACHIEVABLE_HBM_GBS = 6290.0
 SHARE = 512
+CONFIG4_SQUARES = 1024     # BASELINE.json configs[3]: 1024 independent k=128 squares over 1/2/4/8 GPUs
 
 
 def compressions(k: int) -> dict:
@@ -80,9 +81,9 @@ def combined_ceiling(k: int) -> float:
 
 def shard(rank: int, world: int, per_rank: int) -> range:
     """Config 4 (BASELINE.json configs[3]): square indexes of
-    one rank.  Squares are independent, so rank g takes [g*B, (g+1)*B) --
-    with B = 128 and 8 ranks exactly the 1024 squares (seeds 0..1023) of the
-    config, no data-path collective."""
+    one rank.  Squares are independent, so rank g takes [g*B, (g+1)*B) with
+    B = 1024 // world: the 1024 squares (seeds 0..1023) of the config split
+    over the ranks, no data-path collective."""
     return range(rank * per_rank, (rank + 1) * per_rank)
 
 
@@ -229,11 +230,13 @@ def stage_report(st: dict, k: int, batch: int, inplace: bool = False, steps: int
         if steps > 0:
             rec["launches_per_step"] = n / steps
         if name in comp:
+            # compressions x 1 700 nominal int32 lane-ops against
+            # the 78.6 T VALU peak; the compiled-issue-slot view beside it
             c = comp[name] * batch
-            rec.update(bound="valu", achieved=c * SHA_SLOTS / (avg * 1e-3) / 1e12, peak=PEAK_VALU_TOPS,
-                       unit="T issue-slots/s", achieved_instr=c * SHA_INSTR / (avg * 1e-3) / 1e12,
-                       compressions_per_s=c / (avg * 1e-3),
-                       frac_alg=c * ALG_LANE_OPS_PER_COMPRESSION / (avg * 1e-3) / (PEAK_VALU_TOPS * 1e12))
+            rec.update(bound="valu", achieved=c * ALG_LANE_OPS_PER_COMPRESSION / (avg * 1e-3) / 1e12,
+                       peak=PEAK_VALU_TOPS, unit="T int32 lane-ops/s (8(d): 1700 per SHA-256 compression)",
+                       compressions=c, compressions_per_s=c / (avg * 1e-3),
+                       frac_issue_slots=c * SHA_SLOTS / (avg * 1e-3) / 1e12 / PEAK_VALU_TOPS)
         elif name in ("rs_q0", "rs_q3"):
             # rs_q0: read ODS, write Q0|Q1|Q2 (4 k^2 shares); rs_q3: read Q2, write Q3 (2 k^2 shares)
             # (in place there is no Q0 copy: read Q0, write Q1|Q2 = 3 k^2 shares)
@@ -241,9 +244,10 @@ def stage_report(st: dict, k: int, batch: int, inplace: bool = False, steps: int
             rec.update(bound="hbm", achieved=byt / (avg * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")
         if "achieved" in rec:
             rec["frac"] = rec["achieved"] / rec["peak"]
-            ach = ACHIEVABLE_VALU_TOPS if rec["bound"] == "valu" else ACHIEVABLE_HBM_GBS
-            rec["achievable"] = ach
-            rec["frac_of_achievable"] = rec["achieved"] / ach
+            if rec["bound"] == "valu":   # against the measured SHA-256 issue ceiling (tools/sha_probe.hip)
+                rec["frac_of_achievable"] = rec["compressions_per_s"] / ACHIEVABLE_SHA_COMP_S
+            else:
+                rec["frac_of_achievable"] = rec["achieved"] / ACHIEVABLE_HBM_GBS
         out[name] = rec
     return out
 
@@ -273,6 +277,43 @@ def load_pmc(stage: str, field: str = "hbm_bytes_per_launch"):
 
 def load_traffic(stage: str):
     return load_pmc(stage, "hbm_bytes_per_launch")
+
+
+def alg_bytes_per_square(kernel: str, k: int) -> int:
+    """Algorithmic HBM bytes per square of each hot kernel:
+    every input byte read once and every output byte written once.
+      rs_gf8_bs / rs_gf16: 8(d)'s B_RS = 4 k^2 512 (Q0 read, Q1|Q2|Q3 written)
+      nmt_leaves: the EDS read once (W^2 512) + one 96-B leaf slot per cell
+      nmt_levels: every level reads its children and writes its parents,
+                  2W trees x (2W - 2) child slots read + (W - 1) parents, 96 B"""
+    W = 2 * k
+    if kernel in ("rs_gf8_bs", "rs_gf16"):
+        return rs_bytes(k)
+    if kernel == "nmt_leaves":
+        return W * W * (SHARE + 96)
+    if kernel == "nmt_levels":
+        return 2 * W * ((2 * W - 2) + (W - 1)) * 96
+    raise KeyError(kernel)
+
+
+def traffic_report(k: int, squares_per_step: int) -> dict:
+    """Measured HBM bytes (PMC summary, FETCH_SIZE x 2 + WRITE_SIZE, separate
+    rocprofv3 passes of a fixed-shape run: tools/profile_round3.sh) per
+    square and per step of each hot kernel, and their ratio to the
+    algorithmic bytes.  Reproducible from the summary alone:
+    hbm_bytes_per_square = hbm_bytes_per_launch x launches_per_step /
+    squares_per_step of the profiled run (its _config)."""
+    out = {}
+    cfg = load_pmc("_config", "k128" if k == 128 else f"k{k}") or {}
+    for kern in ("rs_gf8_bs" if k <= 128 else "rs_gf16", "nmt_leaves", "nmt_levels"):
+        per_sq = load_pmc(kern, f"hbm_bytes_per_square_k{k}")
+        if per_sq is None:
+            continue
+        alg = alg_bytes_per_square(kern, k)
+        out[kern] = {"hbm_bytes_per_square": per_sq, "traffic_per_step": per_sq * squares_per_step,
+                     "algorithmic_bytes_per_square": alg, "traffic_ratio": per_sq / alg,
+                     "profiled_shape": cfg}
+    return out
 
 
 def cpu_threads(requested: int = 0) -> tuple:
@@ -680,7 +721,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128)
-    ap.add_argument("--batch", type=int, default=128, help="squares per rank per step")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="squares per rank per step (default: config 4's 1024 squares split over the ranks, "
+                         "1024 // world)")
     ap.add_argument("--distinct", type=int, default=0,
                     help="distinct input squares per rank, tiled to the batch (default: all distinct)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -729,18 +772,24 @@ def main():
         dist.destroy_process_group()
         return
 
-    k, B = args.k, args.batch
+    k = args.k
+    # config 4 (BASELINE.json configs[3]): a FIXED workload of 1024 squares
+    # split over the ranks -- rank g takes [g*1024/N, (g+1)*1024/N)
+    B = args.batch if args.batch > 0 else CONFIG4_SQUARES // world
     W = 2 * k
     ctx = Context(local)
 
-    # inputs: config 4's squares of this rank (seeds rank*B .. rank*B+B-1), all
-    # distinct unless --distinct asks for tiling
+    # inputs: this rank's squares, all distinct unless --distinct asks for
+    # tiling; generated on host threads in chunks straight into HBM
     idx = list(shard(rank, world, B))
     nd = B if args.distinct <= 0 else max(1, min(args.distinct, B))
-    base = np.stack([testfactory.random_square(k, i) for i in idx[:nd]])
-    ods_h = np.concatenate([base] * ((B + nd - 1) // nd))[:B] if nd < B else base
-    d_ods = torch.from_numpy(np.ascontiguousarray(ods_h)).to(dev)
-    del base, ods_h
+    d_ods = torch.empty((B, k * k, SHARE), dtype=torch.uint8, device=dev)
+    t_gen = time.perf_counter()
+    for j0, part in testfactory.random_squares(k, idx[:nd]):
+        d_ods[j0:j0 + part.shape[0]].copy_(torch.from_numpy(part))
+    for j in range(nd, B, nd):   # tiling (timing-diagnostic runs only)
+        d_ods[j:j + nd].copy_(d_ods[:min(nd, B - j)])
+    t_gen = time.perf_counter() - t_gen
     d_eds = torch.empty(B * W * W * SHARE, dtype=torch.uint8, device=dev)
     d_rows = torch.empty(B * W * 90, dtype=torch.uint8, device=dev)
     d_cols = torch.empty(B * W * 90, dtype=torch.uint8, device=dev)
@@ -804,14 +853,15 @@ def main():
     stages = stage_report(st, k, B, args.layout == "inplace", n_prof)
     dom = max((s for s in stages if "achieved" in stages[s]), key=lambda s: stages[s]["avg_ms"])
     d = stages[dom]
+    traffic = traffic_report(k, B)
     roofline = {"bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"], "unit": d["unit"],
-                "frac": d["frac"], "traffic": load_traffic(dom), "kernel": dom,
-                "achievable": d["achievable"], "frac_of_achievable": d["frac_of_achievable"]}
-    if "frac_alg" in d:
-        # SURVEY 8(d)'s own definition: compressions x 1700 nominal lane-ops
-        # against the 78.6 T VALU peak (frac above counts compiled issue slots)
-        roofline["frac_alg"] = d["frac_alg"]
-        roofline["achieved_alg_tops"] = d["frac_alg"] * PEAK_VALU_TOPS
+                "frac": d["frac"], "kernel": dom, "launch_ms": d["avg_ms"],
+                "work_per_launch": f"{d.get('compressions', 0)} SHA-256 compressions ({B} squares)",
+                "frac_issue_slots": d.get("frac_issue_slots"), "frac_of_achievable": d["frac_of_achievable"],
+                "traffic": None}
+    if dom in traffic:   # per launch like `achieved`: one launch = the stage pass's whole batch
+        roofline["traffic"] = traffic[dom]["traffic_per_step"]
+        roofline["traffic_ratio"] = traffic[dom]["traffic_ratio"]
     ceiling = combined_ceiling(k)
     roofline["combined_ceiling_squares_per_s"] = ceiling
     roofline["combined_frac"] = (value / world) / ceiling
@@ -821,16 +871,18 @@ def main():
                "unit": "GB/s", "ms_per_step": rs_ms, "algorithmic_bytes_per_step": rs_alg}
     rs_roof["frac"] = rs_roof["achieved"] / rs_roof["peak"]
     rs_roof["achievable"] = ACHIEVABLE_HBM_GBS
-    # measured HBM bytes and VALU instructions of the two RS launches of one
-    # step (PMC summary: per-launch means over rs_q0 and rs_q3)
+    # measured HBM bytes of the RS launches of one step (PMC summary)
     rs_stage = "rs_gf8_bs" if k == 128 else "rs_gf16"
-    t_rs = load_traffic(rs_stage)
-    rs_roof["traffic"] = 2 * t_rs if t_rs else None
-    rs_roof["traffic_ratio"] = rs_roof["traffic"] / rs_alg if t_rs else None
+    if rs_stage in traffic:
+        rs_roof["traffic"] = traffic[rs_stage]["traffic_per_step"]
+        rs_roof["traffic_ratio"] = traffic[rs_stage]["traffic_ratio"]
     rs_roof["frac_of_achievable"] = rs_roof["achieved"] / ACHIEVABLE_HBM_GBS
     v_rs = load_pmc(rs_stage, "SQ_INSTS_VALU")
-    if v_rs:
-        lane = 2 * v_rs * 64 / (rs_ms * 1e-3) / 1e12
+    rs_launches = load_pmc(rs_stage, "launches_per_step_k%d" % k) or 2
+    v_sq = load_pmc("_config", "k%d" % k) or {}
+    if v_rs and v_sq.get("squares_per_step"):
+        # per launch of the profiled shape -> per step of this run
+        lane = v_rs * rs_launches / v_sq["squares_per_step"] * B * 64 / (rs_ms * 1e-3) / 1e12
         rs_roof["valu"] = {"bound": "valu", "achieved": lane, "peak": PEAK_VALU_TOPS, "unit": "T lane-instr/s",
                            "frac": lane / PEAK_VALU_TOPS, "source": "SQ_INSTS_VALU x 64 per step (PMC summary)"}
 
@@ -941,9 +993,14 @@ def main():
         extras["k512"]["rs_roofline"] = {"bound": "hbm", "ms_per_square": rs5,
                                          "achieved": rs_bytes(k5) / (rs5 * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                                          "unit": "GB/s", "frac": rs_bytes(k5) / (rs5 * 1e-3) / 1e9 / PEAK_HBM_GBS}
-        v16 = load_pmc("rs_gf16", "SQ_INSTS_VALU")   # per launch of a one-square profile run
+        v16 = load_pmc("rs_gf16", "SQ_INSTS_VALU")   # per launch of the profiled k=512 run
+        n16 = load_pmc("rs_gf16", "launches_per_step_k512") or 2
+        c16 = (load_pmc("_config", "k512") or {}).get("squares_per_step") or 1
+        t16 = traffic_report(k5, 1)
+        if t16:
+            extras["k512"]["traffic"] = t16
         if v16:
-            lane = 2 * v16 * 64 / (rs5 * 1e-3) / 1e12
+            lane = v16 * n16 / c16 * 64 / (rs5 * 1e-3) / 1e12
             clk = load_pmc("rs_gf16", "effective_clock_ghz") or 2.4
             # a stream with half-rate ops (v_perm) issues one wave64
             # instruction per ~4 cycles per SIMD: 1024 SIMDs x 64 lanes / 4 x clock
@@ -990,16 +1047,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * el / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if B * world == CONFIG4_SQUARES else "weak",
             "vs_baseline": None,
             "dtype": "u8/u32",
             "data": (f"synthetic random-namespace squares (testfactory mirror, SplitMix64), "
                      f"{'all distinct' if nd == B else f'{nd} distinct tiled'}: square indexes "
-                     f"{idx[0]}..{idx[-1]} on rank 0"),
-            "config": {"workload": f"config 4 shard: {B} independent k={k} squares per GPU per step "
-                                   f"(rank g: squares [{B}g, {B}g+{B}); x8 GPUs = config 4's 1024)",
-                       "k": k, "squares_per_gpu_per_step": B, "distinct_squares": nd,
-                       "parallelism": f"dp{world} (independent squares)", "layout": args.layout},
+                     f"{idx[0]}..{idx[-1]} on rank 0 (generated on host threads in {t_gen:.1f} s, "
+                     f"HBM-resident before timing)"),
+            "config": {"workload": (f"config 4: {B * world} independent k={k} squares per step split over "
+                                    f"{world} GPU(s), {B} per GPU (rank g: squares [{B}g, {B}g+{B}))"
+                                    if B * world == CONFIG4_SQUARES else
+                                    f"{B} independent k={k} squares per GPU per step (not config 4's fixed "
+                                    f"1024-square workload)"),
+                       "k": k, "squares_per_step": B * world, "squares_per_gpu_per_step": B,
+                       "distinct_squares": nd, "parallelism": f"dp{world} (independent squares)",
+                       "layout": args.layout},
             "parity": {**parity, "fixture": "tests/golden/config4_k128{,_rest}.json (oracle data roots of squares 0..1023)"},
             "ods_gb_per_s": value * k * k * SHARE / 1e9,
             "stage_pass": {"steps": n_prof, "ms_per_step": 1e3 * el_prof / n_prof,
@@ -1009,6 +1071,7 @@ def main():
                                    "from the event-free timed region with the default two-stream hash split"},
             "roofline": roofline,
             "rs_roofline": rs_roof,
+            "traffic": traffic,
             "stages": stages,
             "cpu_baseline": cpu,
             "extras": extras,

@@ -32,6 +32,7 @@ CDA_ERR_UNSUPPORTED = -7
 CDA_ERR_SQUARE = -8
 CDA_ERR_BYZANTINE = -9
 CDA_ERR_UNREPAIRABLE = -10
+CDA_ERR_COMM = -11
 
 CDA_SQUARE_CONSTRUCT = 0
 CDA_SQUARE_BUILD = 1
@@ -39,7 +40,7 @@ CDA_SQUARE_BUILD = 1
 EXPORTED = (
     "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
     "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
-    "cda_extend_dah_inplace_device",
+    "cda_extend_dah_inplace_device", "cda_reserve",
     "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
@@ -47,7 +48,7 @@ EXPORTED = (
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
     "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
-    "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_extend_dah_split", "cda_split_rows_send",
+    "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_comm_abort", "cda_extend_dah_split", "cda_split_rows_send",
     "cda_extend_dah_multi",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
@@ -114,6 +115,7 @@ def load():
         L.cda_extend_dah_batch.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p, u8p,
                                            C.POINTER(C.c_int32)]
         L.cda_extend_dah_device.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]
+        L.cda_reserve.argtypes = [ctxp, C.c_uint32, C.c_uint32]
         L.cda_extend_dah_inplace_device.argtypes = [ctxp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.cda_rs_encode.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
         L.cda_data_root.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p]
@@ -152,6 +154,7 @@ def load():
         L.cda_comm_unique_id.argtypes = [u8p]
         L.cda_comm_init.argtypes = [ctxp, C.c_int, C.c_int, u8p]
         L.cda_comm_destroy.argtypes = [ctxp]
+        L.cda_comm_abort.argtypes = [ctxp]
         L.cda_extend_dah_split.argtypes = [ctxp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.cda_split_rows_send.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.cda_extend_dah_multi.argtypes = [C.POINTER(ctxp), C.c_uint32, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p,
@@ -221,6 +224,10 @@ class Context:
         self.check(self.lib.cda_extend_dah_device(self.h, d_ods, k, n, d_eds, d_rows, d_cols, d_roots,
                                                   d_status, stream))
 
+    def reserve(self, k: int, n: int):
+        """Pre-size the scratch for device batches of n squares of width k."""
+        self.check(self.lib.cda_reserve(self.h, k, n))
+
     def extend_dah_inplace_device(self, k: int, n: int, d_eds: int, d_rows: int, d_cols: int, d_roots: int,
                                   d_status: int | None = None, stream: int | None = None):
         """As extend_dah_device with the ODS already in Q0 of d_eds (asynchronous)."""
@@ -250,6 +257,10 @@ class Context:
 
     def comm_destroy(self):
         self.check(self.lib.cda_comm_destroy(self.h))
+
+    def comm_abort(self):
+        """ncclCommAbort (safe from a watchdog thread while a call waits)."""
+        self.check(self.lib.cda_comm_abort(self.h))
 
     def extend_dah_split(self, d_rows, k, d_col_block, d_row_roots, d_col_roots, d_root, d_err, stream=None):
         """Config 5 on this rank with the library's own RCCL collectives."""

@@ -123,6 +123,11 @@ class ExtendedDataSquare:
         self.tree_fn = tree_fn
         self._roots = roots
         self._err = err
+        # rsmt2d hashes the cells when RowRoots / ColRoots is first called; the
+        # roots here come from the extension's own GPU submission, so they
+        # hold only while the cells are still the bytes that submission
+        # hashed.  The fingerprint of those bytes is checked on first use.
+        self._fp = _fingerprint(eds) if (roots is not None or err is not None) else None
 
     # -- geometry ---------------------------------------------------------
     def width(self) -> int:
@@ -153,6 +158,13 @@ class ExtendedDataSquare:
 
     # -- roots --------------------------------------------------------------
     def _compute_roots(self):
+        if self._fp is not None:
+            # first use: cells rewritten in place since the extension (same
+            # backing array) invalidate the submission's roots, exactly as
+            # rsmt2d's computeRoots would hash the new bytes
+            if _fingerprint(self._eds) != self._fp:
+                self._roots, self._err = None, None
+            self._fp = None
         if self._roots is None and self._err is None:
             ctx = getattr(self.codec, "ctx", None) or default_context()
             W = self.width()
@@ -219,10 +231,22 @@ class ExtendedDataSquare:
         index = C.c_uint32(0)
         rc = ctx.lib.cda_repair(ctx.h, ptr(self._eds), ptr(pres), W, ptr(rows), ptr(cols), C.byref(axis),
                                 C.byref(index))
-        self._roots, self._err = None, None
+        self._roots, self._err, self._fp = None, None, None
         if rc == _lib.CDA_ERR_BYZANTINE:
             raise ByzantineDataError(rc, ctx.lib.cda_last_error(ctx.h).decode(), axis.value, index.value)
         ctx.check(rc)
+
+
+def _fingerprint(a: np.ndarray) -> bytes:
+    """128-bit content fingerprint of a square's cells (xxh3, ~5 GB/s on one
+    core; blake2b when the xxhash module is absent)."""
+    buf = np.ascontiguousarray(a)
+    try:
+        import xxhash
+        return xxhash.xxh3_128_digest(buf)
+    except ImportError:
+        import hashlib
+        return hashlib.blake2b(buf, digest_size=16).digest()
 
 
 def new_extended_data_square_with_missing(eds: np.ndarray, present: np.ndarray, codec, tree_fn):

@@ -65,3 +65,23 @@ def _sort_rows(a: np.ndarray) -> np.ndarray:
 def random_square(k: int, square_index: int = 0) -> np.ndarray:
     """ODS of width k as (k*k, 512), row-major."""
     return random_namespaced_shares(k * k, square_index)
+
+
+def random_squares(k: int, indexes, threads: int = 0, chunk: int = 64):
+    """Yield (position, (m, k*k, 512) array) chunks of random_square(k, i)
+    for i in `indexes`, generated on a thread pool (numpy releases the GIL in
+    the PRNG and the sort): config 4's 1 024 k = 128 squares take ~40 s on
+    one core.  threads = 0: every CPU of the process's affinity, capped by
+    OMP_NUM_THREADS."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    idx = list(indexes)
+    if threads <= 0:
+        threads = len(os.sched_getaffinity(0))
+        cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        if cap > 0:
+            threads = min(threads, cap)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        for j0 in range(0, len(idx), chunk):
+            part = list(ex.map(lambda i: random_square(k, i), idx[j0:j0 + chunk]))
+            yield j0, np.stack(part)

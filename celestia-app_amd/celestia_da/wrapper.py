@@ -6,8 +6,12 @@ Root (:118-124) and ProveRange (:126-129) hash them on the GPU
 (cda_nmt_axis_root / cda_nmt_prove_range).  A tree handed out by an
 ExtendedDataSquare is pre-seeded with the root the square's own GPU submission
 computed (the cgo drop-in does the same): the seed is used
-only while the tree holds exactly the cells it was seeded for -- a push of
-any other bytes drops it and the root is recomputed from what was pushed.
+only while the tree holds exactly the bytes it was seeded for -- a push of any
+other bytes drops it and the root is recomputed from what was pushed.  Bytes,
+not buffers: seed() keeps a private copy of the seeded cells, so a cell
+rewritten in place after seeding (same backing array) is seen as different;
+the square's own trees are seeded only after ExtendedDataSquare has checked
+its cells against the extension's fingerprint (rsmt2d.py).
 """
 from __future__ import annotations
 
@@ -20,11 +24,6 @@ from ._lib import NAMESPACE_SIZE, NMT_ROOT_SIZE, default_context, ptr
 PARITY_SHARES_NAMESPACE = b"\xff" * NAMESPACE_SIZE   # go-square namespace.ParitySharesNamespace
 EMPTY_ROOT = b"\x00" * (2 * NAMESPACE_SIZE) + bytes.fromhex(
     "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855")  # NmtHasher.EmptyRoot
-
-
-def _addr(x):
-    """Start address of a numpy view's data (None for other objects)."""
-    return x.__array_interface__["data"][0] if isinstance(x, np.ndarray) else None
 
 
 class ErasuredNamespacedMerkleTree:
@@ -61,10 +60,8 @@ class ErasuredNamespacedMerkleTree:
         if self._seed is not None:
             cells = self._seed[1]
             i = self.share_index
-            same = i < len(cells) and (_addr(data) is not None and _addr(data) == _addr(cells[i])
-                                       or bytes(data) == bytes(cells[i]))
-            if not same:
-                self._seed = None   # not the seeded cells: the GPU root is recomputed
+            if not (i < len(cells) and bytes(data) == bytes(cells[i])):
+                self._seed = None   # not the seeded bytes: the GPU root is recomputed
         self._last_ns = ns
         if not isinstance(self._cells, list):
             self._cells = list(self._cells)
@@ -75,13 +72,15 @@ class ErasuredNamespacedMerkleTree:
     # -- seeding (rsmt2d.ExtendedDataSquare) ---------------------------------
     def seed(self, root: bytes, cells):
         """Offer the root the square's GPU submission computed for `cells`;
-        it is used only if exactly these cells are pushed."""
-        self._seed = (root, cells)
+        it is used only if exactly these bytes are pushed (a private copy is
+        kept, so rewriting the caller's buffers afterwards drops the seed)."""
+        self._seed = (root, [bytes(c) for c in cells])
 
     def _seed_root(self, root: bytes, cells):
         """Seed and adopt: the tree holds `cells` (the square's own row or
-        column, already validated by the same submission)."""
-        self.seed(root, cells)
+        column, whose bytes the square has just checked against its
+        extension's fingerprint) and is rooted at once."""
+        self._seed = (root, cells)
         self._cells = cells
         self.share_index = len(cells)
         self._last_ns = PARITY_SHARES_NAMESPACE if len(cells) > self.square_size else None

@@ -207,6 +207,13 @@ int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t 
     });
 }
 
+int cda_reserve(cda_ctx* ctx, uint32_t k, uint32_t n) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (k == 0 || (k & (k - 1)) || k > 1024) return not_pow2(e, k * k);
+        return e.reserve(k, n);
+    });
+}
+
 int cda_extend_dah_inplace_device(cda_ctx* ctx, uint32_t k, uint32_t n, void* d_eds, void* d_row_roots,
                                   void* d_col_roots, void* d_data_roots, int32_t* d_status, void* stream) {
     return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
@@ -593,6 +600,14 @@ int cda_comm_destroy(cda_ctx* ctx) {
     });
 }
 
+int cda_comm_abort(cda_ctx* ctx) {
+    // no context lock: a watchdog thread may call this while another thread
+    // is blocked inside a collective on the same context
+    if (!ctx) return CDA_ERR_INVALID;
+    DeviceScope dev(ctx->eng.device());
+    return ctx->eng.comm_abort();
+}
+
 int cda_split_rows_send(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
                         uint32_t parts, void* d_send, uint32_t* d_err, void* stream) {
     return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
@@ -605,9 +620,9 @@ int cda_split_rows_send(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32
 int cda_extend_dah_split(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, void* d_col_block, void* d_row_roots,
                          void* d_col_roots, void* d_data_root, uint32_t* d_err, void* stream) {
     return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {
-        if (!d_ods_rows || !d_err) return e.fail(CDA_ERR_INVALID, "null buffer");
-        if (e.comm_rank() == 0 && (!d_row_roots || !d_col_roots || !d_data_root))
-            return e.fail(CDA_ERR_INVALID, "null buffer");
+        // per-rank buffer checks happen inside, after this rank has taken part
+        // in every collective (an early return here would leave the peers
+        // blocked in the all-to-all)
         return e.split_extend_dah(static_cast<const uint8_t*>(d_ods_rows), k, static_cast<uint8_t*>(d_col_block),
                                   static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
                                   static_cast<uint8_t*>(d_data_root), d_err, s);

@@ -15,6 +15,7 @@
 // pkg/da/data_availability_header.go:44-75.
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,9 +42,14 @@ __global__ __launch_bounds__(256) void group_rows_kernel(const uint4* __restrict
     dst[(((uint64_t)g * R + r) * C + c) * V + v] = src[i];
 }
 
-int nccl_check(Engine& e, ncclResult_t r, const char* what) {
-    if (r == ncclSuccess) return CDA_OK;
-    return e.fail(CDA_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+// CDA_COMM_FAULT (tests only, read at every split call): make one step fail
+// as if RCCL or the device had failed there -- "a2a" (the all-to-all group),
+// "gather" (the gather group), "local" (this rank's column stage), "alloc"
+// (this rank's scratch allocation in the agreement round).  Lets the GPU
+// tests drive every error path at world size 1.
+bool comm_fault(const char* where) {
+    const char* e = getenv("CDA_COMM_FAULT");
+    return e && strcmp(e, where) == 0;
 }
 
 }  // namespace
@@ -73,95 +79,191 @@ int comm_unique_id(uint8_t* id) {
 
 int Engine::comm_init(int rank, int world, const uint8_t* id) {
     if (world < 1 || rank < 0 || rank >= world) return fail(CDA_ERR_INVALID, "bad rank / world size");
-    if (comm_) {
-        (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
-        comm_ = nullptr;
-    }
+    comm_destroy();
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof uid);
     ncclComm_t c = nullptr;
-    int rc;
-    if ((rc = nccl_check(*this, ncclCommInitRank(&c, world, uid, rank), "ncclCommInitRank"))) return rc;
+    ncclResult_t r = ncclCommInitRank(&c, world, uid, rank);
+    if (r != ncclSuccess) return fail(CDA_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     comm_ = c;
     rank_ = rank;
     world_ = world;
+    comm_k_ = 0;
     return CDA_OK;
 }
 
+// comm_ is swapped out atomically: cda_comm_abort may run on a watchdog
+// thread while another thread holds the context inside a collective.
+void* Engine::take_comm() { return __atomic_exchange_n(&comm_, nullptr, __ATOMIC_ACQ_REL); }
+
 void Engine::comm_destroy() {
-    if (comm_) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
-    comm_ = nullptr;
+    if (void* c = take_comm()) (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
     rank_ = 0;
     world_ = 0;
+    comm_k_ = 0;
 }
 
+// An RCCL call failed: the communicator may hold half-posted operations, so it
+// is aborted (ncclCommAbort also stops this rank's queued collective kernels)
+// and released.  Peers blocked in the same collective are released by their
+// own host calling cda_comm_abort (e.g. on a timeout), as NCCL prescribes.
+int Engine::comm_fail(const char* what, int result) {
+    std::string msg = std::string(what) + ": " + ncclGetErrorString(static_cast<ncclResult_t>(result)) +
+                      " (communicator aborted; every rank must call cda_comm_init again)";
+    if (void* c = take_comm()) (void)ncclCommAbort(static_cast<ncclComm_t>(c));
+    rank_ = 0;
+    world_ = 0;
+    comm_k_ = 0;
+    return fail(CDA_ERR_COMM, msg);
+}
+
+int Engine::comm_abort() {
+    if (void* c = take_comm()) (void)ncclCommAbort(static_cast<ncclComm_t>(c));
+    return CDA_OK;
+}
+
+// Config 5 on this rank.  Error discipline (every rank must leave every
+// collective it entered, or its peers block forever):
+//   * checks that depend only on k and the world size fail on every rank alike
+//     before any collective;
+//   * scratch is allocated when k changes, followed by one agreement
+//     all-reduce (MIN of an ok flag, read back on the host): if any rank could
+//     not allocate, every rank returns CDA_ERR_OOM and the communicator stays
+//     usable;
+//   * a local failure after that (a kernel launch, bad per-rank buffers) does
+//     not return early: the rank stops its own compute, poisons its push-order
+//     word with 0 (never a valid violation word: positions start at 1), takes
+//     part in the remaining collectives and returns its error at the end; rank
+//     0 then finds 0 in the MIN-reduced word and skips the combine;
+//   * an RCCL call that fails closes its group (ncclGroupEnd), aborts the
+//     communicator and returns CDA_ERR_COMM.
 int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_block, uint8_t* d_row_roots,
                              uint8_t* d_col_roots, uint8_t* d_root, uint32_t* d_err, hipStream_t s) {
     if (!comm_) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
     const uint32_t G = (uint32_t)world_, W = 2 * k;
-    if (k == 0 || (k & (k - 1)) || (G & (G - 1)) || k % G) return fail(CDA_ERR_INVALID, "world size must divide k");
+    if (k == 0 || (k & (k - 1)) || (G & (G - 1)) || k % G || k > 1024)
+        return fail(CDA_ERR_INVALID, "world size must divide k (a power of two <= 1024)");
     const uint32_t R = k / G, C = W / G;
     const size_t piece = (size_t)R * C * kShare;   // one rank pair's all-to-all block
-    ncclComm_t comm = static_cast<ncclComm_t>(comm_);
+    const size_t own = (size_t)(C + W) * kSlot, all = (size_t)G * (C + W) * kSlot;
+    ncclComm_t comm = static_cast<ncclComm_t>(__atomic_load_n(&comm_, __ATOMIC_ACQUIRE));
+    if (!comm) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
+    ncclResult_t r;
     int rc;
-    if (G > 1 && (rc = check(split_send_.ensure(piece * G), "hipMalloc send"))) return rc;
-    uint8_t* block = d_col_block;
-    if (!block) {
-        if ((rc = check(split_col_.ensure((size_t)W * C * kShare), "hipMalloc column block"))) return rc;
-        block = split_col_.as<uint8_t>();
+    // -- scratch + agreement (only when k changes; k is the same on every rank) --
+    if (comm_k_ != k) {
+        int ok = 1;
+        if (comm_fault("alloc")) ok = 0;
+        if (ok && G > 1 && split_send_.ensure(piece * G) != hipSuccess) ok = 0;
+        if (ok && split_col_.ensure((size_t)W * C * kShare) != hipSuccess) ok = 0;
+        if (ok && split_slots_.ensure(own + all + 64) != hipSuccess) ok = 0;
+        // the column stage's leaf / level slots too, so no buffer grows (and
+        // synchronises) once the collectives are queued
+        if (ok && leaf_.ensure((size_t)W * C * kSlot) != hipSuccess) ok = 0;
+        if (ok && lvl_.ensure((size_t)W * C * kSlot) != hipSuccess) ok = 0;
+        (void)hipGetLastError();
+        if ((rc = check(comm_flag_.ensure(4), "hipMalloc agreement word"))) return rc;
+        int32_t* d_ok = comm_flag_.as<int32_t>();
+        int32_t h_ok = ok;
+        if ((rc = check(hipMemcpyAsync(d_ok, &h_ok, 4, hipMemcpyHostToDevice, s), "H2D agreement word"))) return rc;
+        if ((r = ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, comm, s)) != ncclSuccess)
+            return comm_fail("ncclAllReduce (allocation agreement)", r);
+        if ((rc = check(hipMemcpyAsync(&h_ok, d_ok, 4, hipMemcpyDeviceToHost, s), "D2H agreement word"))) return rc;
+        if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+        if (!h_ok)
+            return fail(CDA_ERR_OOM, ok ? "a peer rank could not allocate its split scratch"
+                                        : "split scratch allocation failed on this rank");
+        comm_k_ = k;
     }
+    uint8_t* block = d_col_block ? d_col_block : split_col_.as<uint8_t>();
     // slots: this rank's column roots [C] and row subtrees [W]; rank 0 also
     // the gathered [G][W] subtrees and [W] column roots (rank order)
-    const size_t own = (size_t)(C + W) * kSlot, all = (size_t)G * (C + W) * kSlot;
-    if ((rc = check(split_slots_.ensure(own + all), "hipMalloc slots"))) return rc;
     uint8_t* col_slots = split_slots_.as<uint8_t>();
     uint8_t* row_sub = col_slots + (size_t)C * kSlot;
     uint8_t* g_sub = col_slots + own;                        // [G][W][96]
     uint8_t* g_col = g_sub + (size_t)G * W * kSlot;          // [G*C = W][96]
-    if ((rc = check(hipMemsetAsync(d_err, 0xFF, 4, s), "hipMemsetAsync"))) return rc;
+    // the push-order word: the caller's, or library scratch when it passed none
+    uint32_t* err = d_err ? d_err : reinterpret_cast<uint32_t*>(g_col + (size_t)W * kSlot);
+    int local = CDA_OK;                                      // first local failure
+    std::string local_msg;
+    auto local_fail = [&](int code, const std::string& msg) {
+        if (local == CDA_OK) {
+            local = code;
+            local_msg = msg;
+        }
+    };
+    if (!d_rows || !d_err) local_fail(CDA_ERR_INVALID, "null buffer");
+    if (rank_ == 0 && (!d_row_roots || !d_col_roots || !d_root)) local_fail(CDA_ERR_INVALID, "null buffer");
+    if (hipMemsetAsync(err, local ? 0x00 : 0xFF, 4, s) != hipSuccess) return comm_fail("hipMemsetAsync", ncclUnhandledCudaError);
+    // a local step: runs only while this rank is healthy; a failure poisons
+    // the push-order word and keeps the rank in the collectives
+    auto step = [&](auto&& f) -> bool {
+        if (local != CDA_OK) return true;
+        const int e = f();
+        if (e == CDA_OK) return true;
+        local_fail(e, last_error());
+        return hipMemsetAsync(err, 0x00, 4, s) == hipSuccess;
+    };
+    auto grouped = [&](const char* what, auto&& post) -> int {
+        if ((r = ncclGroupStart()) != ncclSuccess) return comm_fail(what, r);
+        const ncclResult_t first = post();
+        const ncclResult_t end = ncclGroupEnd();   // always closed, even after a failed post
+        if (first != ncclSuccess) return comm_fail(what, first);
+        if (end != ncclSuccess) return comm_fail(what, end);
+        return CDA_OK;
+    };
     if (G == 1) {
         // one rank: the row block IS rows 0..k-1 of the (whole) column block
-        if ((rc = enqueue_split_rows_send(d_rows, k, R, 0, 1, block, d_err, s))) return rc;
+        if (!step([&] { return enqueue_split_rows_send(d_rows, k, R, 0, 1, block, err, s); }))
+            return comm_fail("poison", ncclUnhandledCudaError);
     } else {
         // 1. rows -> [G][R][C] send layout
-        if ((rc = enqueue_split_rows_send(d_rows, k, R, (uint32_t)rank_ * R, G, split_send_.as<uint8_t>(), d_err,
-                                          s)))
-            return rc;
+        if (!step([&] {
+                return enqueue_split_rows_send(d_rows, k, R, (uint32_t)rank_ * R, G, split_send_.as<uint8_t>(), err, s);
+            }))
+            return comm_fail("poison", ncclUnhandledCudaError);
         // 2. all-to-all: piece h goes to rank h; rank g's piece lands at rows
         //    g*R..g*R+R-1 of the column block
-        if ((rc = nccl_check(*this, ncclGroupStart(), "ncclGroupStart"))) return rc;
-        for (uint32_t h = 0; h < G; h++) {
-            if ((rc = nccl_check(*this,
-                                 ncclSend(split_send_.as<uint8_t>() + h * piece, piece, ncclUint8, (int)h, comm, s),
-                                 "ncclSend")))
-                return rc;
-            if ((rc = nccl_check(*this, ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s), "ncclRecv")))
-                return rc;
-        }
-        if ((rc = nccl_check(*this, ncclGroupEnd(), "ncclGroupEnd"))) return rc;
+        if ((rc = grouped("all-to-all", [&]() -> ncclResult_t {
+                 if (comm_fault("a2a")) return ncclInternalError;
+                 for (uint32_t h = 0; h < G; h++) {
+                     ncclResult_t q = ncclSend(split_send_.as<uint8_t>() + h * piece, piece, ncclUint8, (int)h, comm, s);
+                     if (q != ncclSuccess) return q;
+                     if ((q = ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s)) != ncclSuccess) return q;
+                 }
+                 return ncclSuccess;
+             })))
+            return rc;
     }
     // 3. columns: Q2|Q3 parity, leaves, column roots, row subtrees
-    if ((rc = enqueue_split_cols(block, k, C, (uint32_t)rank_ * C, col_slots, row_sub, d_err, s))) return rc;
+    if (!step([&] {
+            if (comm_fault("local")) return fail(CDA_ERR_DEVICE, "column stage: injected fault (CDA_COMM_FAULT=local)");
+            return enqueue_split_cols(block, k, C, (uint32_t)rank_ * C, col_slots, row_sub, err, s);
+        }))
+        return comm_fail("poison", ncclUnhandledCudaError);
     // 4. gather the slots on rank 0 and reduce the push-order word
-    if ((rc = nccl_check(*this, ncclGroupStart(), "ncclGroupStart"))) return rc;
-    if (rank_ == 0) {
-        for (uint32_t h = 0; h < G; h++) {
-            if ((rc = nccl_check(*this, ncclRecv(g_sub + (size_t)h * W * kSlot, (size_t)W * kSlot, ncclUint8, (int)h,
-                                                 comm, s),
-                                 "ncclRecv")))
-                return rc;
-            if ((rc = nccl_check(*this, ncclRecv(g_col + (size_t)h * C * kSlot, (size_t)C * kSlot, ncclUint8, (int)h,
-                                                 comm, s),
-                                 "ncclRecv")))
-                return rc;
-        }
-    }
-    if ((rc = nccl_check(*this, ncclSend(row_sub, (size_t)W * kSlot, ncclUint8, 0, comm, s), "ncclSend"))) return rc;
-    if ((rc = nccl_check(*this, ncclSend(col_slots, (size_t)C * kSlot, ncclUint8, 0, comm, s), "ncclSend"))) return rc;
-    if ((rc = nccl_check(*this, ncclGroupEnd(), "ncclGroupEnd"))) return rc;
-    if ((rc = nccl_check(*this, ncclReduce(d_err, d_err, 1, ncclUint32, ncclMin, 0, comm, s), "ncclReduce")))
+    if ((rc = grouped("gather", [&]() -> ncclResult_t {
+             if (comm_fault("gather")) return ncclInternalError;
+             ncclResult_t q;
+             if (rank_ == 0) {
+                 for (uint32_t h = 0; h < G; h++) {
+                     if ((q = ncclRecv(g_sub + (size_t)h * W * kSlot, (size_t)W * kSlot, ncclUint8, (int)h, comm, s)) !=
+                         ncclSuccess)
+                         return q;
+                     if ((q = ncclRecv(g_col + (size_t)h * C * kSlot, (size_t)C * kSlot, ncclUint8, (int)h, comm, s)) !=
+                         ncclSuccess)
+                         return q;
+                 }
+             }
+             if ((q = ncclSend(row_sub, (size_t)W * kSlot, ncclUint8, 0, comm, s)) != ncclSuccess) return q;
+             return ncclSend(col_slots, (size_t)C * kSlot, ncclUint8, 0, comm, s);
+         })))
         return rc;
-    // 5. rank 0: top log2(G) levels of every row tree, roots, data root
+    if ((r = ncclReduce(err, err, 1, ncclUint32, ncclMin, 0, comm, s)) != ncclSuccess) return comm_fail("ncclReduce", r);
+    if (local != CDA_OK) return fail(local, local_msg);
+    // 5. rank 0: top log2(G) levels of every row tree, roots, data root (a
+    //    peer that failed left 0 in the reduced word: the combine still runs on
+    //    whatever arrived, and the caller sees d_err == 0)
     if (rank_ == 0) return enqueue_split_combine(g_sub, G, k, g_col, d_row_roots, d_col_roots, d_root, s);
     return CDA_OK;
 }

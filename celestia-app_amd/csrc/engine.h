@@ -119,6 +119,9 @@ class Engine {
     // d_status (optional): n int32 CDA_OK / CDA_ERR_PUSH_ORDER.
     int enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
                            uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s);
+    // Size the device batch calls' scratch for n squares of width k, so later
+    // calls up to that size never grow (and synchronise) a buffer.
+    int reserve(uint32_t k, uint32_t n);
     // RS extension only (ExtendShares).
     // err_init (optional): n push-order words set to ~0 by the first RS launch.
     int enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, hipStream_t s,
@@ -144,6 +147,7 @@ class Engine {
                                 uint8_t* d_send, uint32_t* d_err, hipStream_t s);
     int comm_init(int rank, int world, const uint8_t* id);
     void comm_destroy();
+    int comm_abort();   // ncclCommAbort (e.g. from a host watchdog after a peer failed)
     int comm_rank() const { return rank_; }
     int split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_block, uint8_t* d_row_roots,
                          uint8_t* d_col_roots, uint8_t* d_root, uint32_t* d_err, hipStream_t s);
@@ -222,6 +226,13 @@ class Engine {
 
   private:
     int check(hipError_t e, const char* what);
+    // stages enqueued since the context's work was last seen complete (for
+    // attributing asynchronous device faults; see check())
+    static constexpr size_t kMaxPending = 48;
+    std::vector<const char*> pending_;
+    bool sync_check_ = false;   // CDA_SYNC_CHECK: synchronise after every stage
+    void note_stage(const char* what);
+    std::string pending_stages() const;
     // levels of the forests down to `stop` nodes per tree (f[i].in then
     // describes that level); stop = 1 runs them all
     int run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
@@ -317,7 +328,10 @@ class Engine {
     // send buffer, column block, slots
     void* comm_ = nullptr;
     int rank_ = 0, world_ = 0;
-    DevBuf split_blk_, split_send_, split_col_, split_slots_;
+    uint32_t comm_k_ = 0;   // k whose split scratch every rank agreed on (0 = none yet)
+    DevBuf split_blk_, split_send_, split_col_, split_slots_, comm_flag_;
+    int comm_fail(const char* what, int nccl_result);
+    void* take_comm();   // abort + release the communicator, CDA_ERR_COMM
     int build_trees(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees, uint32_t square_size,
                     const uint32_t* axis, std::vector<uint64_t>* level_off, std::vector<uint32_t>* err_out);
     int tree_order_error(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,

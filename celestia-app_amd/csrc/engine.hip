@@ -26,8 +26,10 @@ namespace cda {
 hipError_t DevBuf::ensure(size_t n) {
     if (n <= bytes && ptr) return hipSuccess;
     // Growing: queued work (any stream) may still read the old buffer, so the
-    // device drains before it is freed.  Buffers only grow, so this happens a
-    // handful of times per context.
+    // device drains before it is freed (hipFree synchronises the device in HIP
+    // anyway).  Buffers only grow, so this happens a handful of times per
+    // context; a caller that needs every device entry point to stay
+    // enqueue-only sizes the scratch once up front (cda_reserve).
     if (ptr) (void)hipDeviceSynchronize();
     release();
     size_t want = n < 256 ? 256 : n;
@@ -56,7 +58,8 @@ Engine::~Engine() {
                       &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_, &cm_plan_, &cm_tables_,
                       &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_, &gf8_log_, &gf8_exp_, &gf8_skew_, &rp_cw_,
                       &rp_err_, &rp_present_, &rp_parity_, &rp_buf_, &rp_flags_, &tr_cells_, &tr_levels_,
-                      &tr_axis_, &tr_roots_, &rs_pad_, &split_blk_, &split_send_, &split_col_, &split_slots_})
+                      &tr_axis_, &tr_roots_, &rs_pad_, &split_blk_, &split_send_, &split_col_, &split_slots_,
+                      &comm_flag_})
         b->release();
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);
@@ -81,12 +84,63 @@ Engine::~Engine() {
         if (q) (void)hipStreamDestroy(q);
 }
 
+// Kernel faults surface asynchronously: at the next launch, copy or
+// synchronisation of the context, whatever stage that is.  check() therefore
+// keeps the stages enqueued since the context's work was last seen complete
+// (pending_), and an asynchronous fault names them instead of blaming the
+// stage that happened to detect it.  CDA_SYNC_CHECK=1 synchronises after every
+// successful stage, so a fault is reported by the stage that raised it.
+static bool async_fault(hipError_t e) {
+    return e == hipErrorIllegalAddress || e == hipErrorLaunchTimeOut || e == hipErrorAssert ||
+           e == hipErrorLaunchFailure;
+}
+
+static bool is_sync_point(const char* what) {
+    return strncmp(what, "hipStreamSynchronize", 20) == 0 || strncmp(what, "hipEventSynchronize", 19) == 0 ||
+           strncmp(what, "hipDeviceSynchronize", 20) == 0;
+}
+
+void Engine::note_stage(const char* what) {
+    if (is_sync_point(what)) {   // everything enqueued before completed cleanly
+        pending_.clear();
+        return;
+    }
+    if (!pending_.empty() && strcmp(pending_.back(), what) == 0) return;
+    if (pending_.size() >= kMaxPending) pending_.erase(pending_.begin());
+    pending_.push_back(what);
+}
+
+std::string Engine::pending_stages() const {
+    std::string s;
+    for (const char* p : pending_) {
+        if (!s.empty()) s += " -> ";
+        s += p;
+    }
+    return s.empty() ? std::string("none recorded") : s;
+}
+
 int Engine::check(hipError_t e, const char* what) {
-    if (e == hipSuccess) return CDA_OK;
-    char buf[256];
-    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    if (e == hipSuccess) {
+        if (sync_check_ && !is_sync_point(what)) {
+            const hipError_t f = hipDeviceSynchronize();
+            if (f != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(CDA_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(f) +
+                                                " (CDA_SYNC_CHECK: raised by this stage)");
+            }
+            pending_.clear();
+            return CDA_OK;
+        }
+        note_stage(what);
+        return CDA_OK;
+    }
+    std::string msg = std::string(what) + ": " + hipGetErrorString(e);
+    if (async_fault(e))
+        msg += " (asynchronous device fault, detected here but raised by GPU work of this context not yet seen "
+               "complete; stages enqueued since, oldest first: " +
+               pending_stages() + "; set CDA_SYNC_CHECK=1 to name the faulting stage)";
     (void)hipGetLastError();  // clear sticky launch error state
-    return fail(e == hipErrorOutOfMemory ? CDA_ERR_OOM : CDA_ERR_DEVICE, buf);
+    return fail(e == hipErrorOutOfMemory ? CDA_ERR_OOM : CDA_ERR_DEVICE, msg);
 }
 
 int Engine::init() {
@@ -118,6 +172,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -191,7 +246,11 @@ uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n) const {
 }
 
 void Engine::order_begin(hipStream_t s) {
-    if (order_used_) (void)hipStreamWaitEvent(s, order_ev_, 0);
+    if (!order_used_) return;
+    // the previous calls' work is complete (without a fault): nothing of it can
+    // surface later
+    if (hipEventQuery(order_ev_) == hipSuccess) pending_.clear();
+    (void)hipStreamWaitEvent(s, order_ev_, 0);
 }
 
 void Engine::order_end(hipStream_t s) {
@@ -296,6 +355,13 @@ int Engine::dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s) 
     if ((rc = check(root_slots_.ensure((size_t)n * 2 * W * kSlot), "hipMalloc root slots"))) return rc;
     if ((rc = check(dig_.ensure((size_t)n * 2 * W * 32), "hipMalloc digests"))) return rc;
     return d_err ? check(hipMemsetAsync(d_err, 0xFF, (size_t)n * 4, s), "hipMemsetAsync") : CDA_OK;
+}
+
+int Engine::reserve(uint32_t k, uint32_t n) {
+    int rc;
+    if (!err_words(n)) return fail(CDA_ERR_OOM, "hipMalloc err words");
+    if ((rc = dah_prepare(2 * k, n, nullptr, stream_))) return rc;
+    return check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 // Row trees: leaves (t, i); column trees: leaves (i, t) of the same leaf grid.
@@ -735,8 +801,14 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
         }
     };
     std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; t++) th.emplace_back(part, t);
+    unsigned started = 1;   // parts [0, started) have a thread (part 0: the caller)
+    try {
+        th.reserve(nt);
+        for (unsigned t = 1; t < nt; t++, started++) th.emplace_back(part, t);
+    } catch (...) {   // no more threads (std::system_error) or memory: copy the rest here
+    }
     part(0);
+    for (unsigned t = started; t < nt; t++) part(t);
     for (auto& x : th) x.join();
 }
 

@@ -37,10 +37,6 @@
 
 #include "cda_kernels.h"
 
-#ifndef CDA_RS16_PROBE
-#define CDA_RS16_PROBE 0
-#endif
-
 namespace cda {
 
 namespace {
@@ -385,57 +381,14 @@ constexpr uint32_t cw_lds_bytes() {
 #endif
 }
 
-// Timing-diagnostic builds only (tools/rs16_phase_probe.sh, wrong output):
-// CDA_RS16_PROBE=1 drops the butterfly layers (memory + exchanges alone),
-// =2 drops the global loads and stores (compute + exchanges alone),
-// =3 gives every wave wave 0's pass-A / A' constants (scalar-cache hits),
-// =4 stores one dword per lane and parity shard (half the stores),
-// =5 stores no parity (loads kept), =6 drops the exchanges' barriers
-// (timing only, wrong output).  (Dropping the per-group lgkmcnt wait is not a
-// valid probe: an s_load still in flight lands in SGPRs the compiler has
-// reused -- tried once, it faulted.)
-constexpr bool kRs16Compute = CDA_RS16_PROBE != 1, kRs16Memory = CDA_RS16_PROBE != 2;
 
 }  // namespace
-
-// Timeline builds only (tools/rs16_trace.sh): CDA_RS16_TRACE=1 has every wave
-// record the 100 MHz device clock at each phase boundary (slots 0-7) and its
-// XCC / HW_ID (9); =2 also waits for the data loads before pass A (slot 10);
-// CDA_RS16_TRACE_MASK selects slots.  Index: Q0 launch
-// (1024 codewords per square) from 0, Q2 launch (512) from kTrQ2.
-#ifndef CDA_RS16_TRACE
-#define CDA_RS16_TRACE 0
-#endif
-#ifndef CDA_RS16_TRACE_MASK
-#define CDA_RS16_TRACE_MASK 0xFFF
-#endif
-#if CDA_RS16_TRACE
-constexpr uint32_t kTrSlots = 12, kTrWgs = 12288, kTrQ2 = 8192;   // up to 8 squares
-__device__ unsigned long long g_rs16_trace[kTrWgs][kTrSlots][16];   // [workgroup][slot][wave]
-#endif
 
 namespace {
 
 template <int K>
 __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restrict__ tab, const RsJob job) {
     rs_err_init(job);
-#if CDA_RS16_TRACE
-    // one clock read + one store per wave and mark, the same address and value
-    // from every lane (no branch, so the marks do not split the schedule)
-    const uint32_t tr_i = (gridDim.x == 512 ? kTrQ2 : 0u) + blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t tr_w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    auto mark = [&](uint32_t slot, uint32_t = 0) {
-        if (!((CDA_RS16_TRACE_MASK >> slot) & 1)) return;
-        unsigned long long t;
-        asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-        g_rs16_trace[tr_i][slot][tr_w] = t;
-    };
-    mark(0);
-    g_rs16_trace[tr_i][9][tr_w] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
-                                  __builtin_amdgcn_s_getreg((31 << 11) | 4);
-#else
-    auto mark = [](uint32_t, uint32_t = 0) {};
-#endif
     extern __shared__ uint32_t X[];
     constexpr int S = K / 16;      // shards per lane in pass A
     constexpr int R = S / 16;      // residues per wave in pass B
@@ -458,7 +411,6 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         __syncthreads();
     }
 #endif
-    mark(1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t off = 64 * (lane >> 3) + 4 * (lane & 7);    // lo dword; hi at +32
@@ -496,10 +448,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     // they become residue R*jj + q's shard t -- in place, so pass B's
     // residue q lives in registers {R*t + q}.
     uint32_t lo[S], hi[S];
-    // exchange barrier (CDA_RS16_PROBE == 6: none -- timing probe only)
-    auto xbar = [] {
-        if constexpr (CDA_RS16_PROBE != 6) __syncthreads();
-    };
+    auto xbar = [] { __syncthreads(); };
     auto xchg_a_to_b = [&]() {
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
@@ -537,34 +486,20 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
 
     // ---------------- pass A: IFFT d = 1 .. S/2 -------------------------
     const uint32_t base = S * wave;
-    if constexpr (kRs16Memory) {
-        sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (base + jj.value) * ss, lo[jj.value], hi[jj.value]); });
-    } else {
-        sfor<0, S, 1>([&](auto jj) {
-            lo[jj.value] = (threadIdx.x + 977u * blockIdx.x) * (2u * jj.value + 1u);
-            hi[jj.value] = lo[jj.value] ^ 0x5bd1e995u;
-        });
-    }
-    if (kRs16Memory && c0 != kNoCopy) {
+    sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (base + jj.value) * ss, lo[jj.value], hi[jj.value]); });
+    if (c0 != kNoCopy) {
         sfor<0, S, 1>([&](auto jj) { st(E, c0 + (base + jj.value) * g.cpy_sh, lo[jj.value], hi[jj.value]); });
     }
-#if CDA_RS16_TRACE == 2
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    mark(10);
-#endif
     // `base` is re-laundered per table index (like lane_off) so the compiler
     // does not precompute all S-1 group addresses up front and spill them
     auto wave_base = [&]() {
-        uint32_t b = CDA_RS16_PROBE == 3 ? 0u : base;
+        uint32_t b = base;
         asm volatile("" : "+s"(b));
         return b;
     };
-    if constexpr (kRs16Compute)
-        ifft_regs<S>(lo, hi, T, TB + 8 * S * (CDA_RS16_PROBE == 3 ? 0u : wave), [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); },
+    ifft_regs<S>(lo, hi, T, TB + 8 * S * wave, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); },
                      [](int g, int d) { return (uint32_t)(K - 1 + g + d); });
-    mark(2);
     xchg_a_to_b();
-    mark(3);
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
     // residue R*wave + q: shards R*wave + q + S*t in registers R*t + q
     // all R residues go through each butterfly group together (same constants)
@@ -577,13 +512,10 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
                 hr[16 * q + tt.value] = hi[R * tt.value + q];
             });
         });
-        if constexpr (kRs16Compute) {
-            layers_regs<16, true, false, R>(lr, hr, T, TB,
-                                            [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
-            layers_regs<16, false, true, R>(lr, hr, T, TB,
-                                            [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
-        }
-        mark(4);
+        layers_regs<16, true, false, R>(lr, hr, T, TB,
+                                        [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
+        layers_regs<16, false, true, R>(lr, hr, T, TB,
+                                        [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
             sfor<0, 16, 1>([&](auto tt) {
@@ -593,32 +525,11 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         });
     }
     xchg_b_to_a();
-    mark(5);
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
     // parity shard j is stored as soon as its last butterfly is done
-    auto store_j = [&](auto jj) {
-        if constexpr (CDA_RS16_PROBE == 4) {   // timing probe: the lo dwords only (half the stores)
-            uint8_t* p = E + d0 + (base + jj.value) * ds;
-            *reinterpret_cast<uint32_t*>(p + off) = lo[jj.value] ^ hi[jj.value];
-        } else if constexpr (CDA_RS16_PROBE == 5) {   // timing probe: no parity stores at all
-            if ((lo[jj.value] ^ hi[jj.value]) == 0x9E3779B9u && threadIdx.x == 1023u) E[d0] = 1;
-        } else if constexpr (kRs16Memory) {
-            st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]);
-        }
-    };
-    if constexpr (kRs16Compute)
-        fft_regs<S>(lo, hi, T, TB + 8 * S * (CDA_RS16_PROBE == 3 ? 0u : wave), [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); },
-                    store_j, [](int g, int d) { return (uint32_t)(g + d - 1); });
-    mark(6);
-    if constexpr (!kRs16Memory) {   // keep every result live: a store no input can trigger
-        uint32_t acc = 0;
-        sfor<0, S, 1>([&](auto jj) { acc ^= (lo[jj.value] + hi[jj.value]) * (2u * jj.value + 1u); });
-        if (acc == 0x9E3779B9u && threadIdx.x == 1023u) E[d0] = (uint8_t)acc;
-        return;
-    }
-    if constexpr (!kRs16Compute)
-        sfor<0, S, 1>([&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); });
-    mark(7);
+    auto store_j = [&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); };
+    fft_regs<S>(lo, hi, T, TB + 8 * S * wave, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); },
+                store_j, [](int g, int d) { return (uint32_t)(g + d - 1); });
 }
 
 // ---------------------------------------------------------------------------
@@ -728,12 +639,6 @@ hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s
 
 }  // namespace
 
-#if CDA_RS16_TRACE
-extern "C" int cda_debug_rs16_trace(void* host, size_t bytes) {
-    if (bytes > sizeof(g_rs16_trace)) bytes = sizeof(g_rs16_trace);
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rs16_trace), bytes) == hipSuccess ? 0 : -1;
-}
-#endif
 
 hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s);
 

@@ -89,8 +89,10 @@ enum {
     CDA_ERR_UNSUPPORTED = -7,   /* shard count the codec does not support */
     CDA_ERR_SQUARE = -8,        /* go-square square.Construct / Build error (message from cda_last_error) */
     CDA_ERR_BYZANTINE = -9,     /* rsmt2d ErrByzantineData ("byzantine row: %d" / "byzantine col: %d") */
-    CDA_ERR_UNREPAIRABLE = -10  /* rsmt2d ErrUnrepairableDataSquare ("failed to solve data square") /
+    CDA_ERR_UNREPAIRABLE = -10, /* rsmt2d ErrUnrepairableDataSquare ("failed to solve data square") /
                                    reedsolomon ErrTooFewShards */
+    CDA_ERR_COMM = -11          /* an RCCL call failed: the context's communicator was aborted and
+                                   released; every rank must call cda_comm_init again */
 };
 
 typedef struct cda_ctx cda_ctx;
@@ -137,6 +139,12 @@ int cda_extend_dah_batch(cda_ctx *ctx, const uint8_t *ods, uint32_t k, uint32_t 
  * (n int32, device memory, may be NULL). */
 int cda_extend_dah_device(cda_ctx *ctx, const void *d_ods, uint32_t k, uint32_t n, void *d_eds, void *d_row_roots,
                           void *d_col_roots, void *d_data_roots, int32_t *d_status, void *stream);
+
+/* Size the context's scratch for device batches of up to n squares of width
+ * k (synchronous).  Scratch buffers only grow, and growing one drains the
+ * device first (hipFree does); after cda_reserve the device entry points for
+ * batches up to that size stay purely enqueue-only. */
+int cda_reserve(cda_ctx *ctx, uint32_t k, uint32_t n);
 
 /* As cda_extend_dah_device, but the k*k ODS shares are already in place in
  * quadrant Q0 of d_eds (row r, column c at (r*2k + c)*512 of each square),
@@ -201,11 +209,24 @@ int cda_split_combine(cda_ctx *ctx, const void *d_row_subtree_slots, uint32_t pa
  *     columns [rank*C, rank*C + C) on return (row-major [W][C][512]);
  *   d_row_roots / d_col_roots (W*90) / d_data_root (32): rank 0 only;
  *   d_err: one device uint32, on rank 0 the MIN over ranks of the push-order
- *     words (0xFFFFFFFF = ordered; axis<<24 | index<<12 | position). */
+ *     words (0xFFFFFFFF = ordered; axis<<24 | index<<12 | position; 0 = a rank
+ *     failed locally and the outputs are invalid). */
 #define CDA_COMM_ID_BYTES 128
 int cda_comm_unique_id(uint8_t id[CDA_COMM_ID_BYTES]);
 int cda_comm_init(cda_ctx *ctx, int rank, int world, const uint8_t id[CDA_COMM_ID_BYTES]);
 int cda_comm_destroy(cda_ctx *ctx);
+/* ncclCommAbort of the context's communicator (then released).  Takes no
+ * context lock, so a host watchdog may call it from another thread while a
+ * call on the context waits in a collective for a peer that failed.  Errors
+ * of cda_extend_dah_split: checks that depend on k / the world size fail on
+ * every rank before any collective; scratch is sized when k changes, followed
+ * by one agreement all-reduce, so an allocation failure on any rank makes
+ * every rank return CDA_ERR_OOM; a local failure after that keeps the rank in
+ * the remaining collectives with its push-order word poisoned to 0 (rank 0's
+ * reduced d_err is then 0: the outputs are invalid) and returns the rank's
+ * error; a failed RCCL call closes its group, aborts the communicator and
+ * returns CDA_ERR_COMM. */
+int cda_comm_abort(cda_ctx *ctx);
 int cda_extend_dah_split(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, void *d_col_block, void *d_row_roots,
                          void *d_col_roots, void *d_data_root, uint32_t *d_err, void *stream);
 /* Step 1 of the split for a caller that runs its own all-to-all (e.g. over

@@ -87,6 +87,50 @@ def test_config4_other_rank_shard_on_gpu(ctx, rank):
         assert _sha(c[j].reshape(W, 90)) == want["col_roots_sha256"], i
 
 
+@pytest.mark.gpu
+def test_config4_all_1024_squares_one_submission(ctx):
+    """Config 4 as BASELINE.json configs[3] defines it at N = 1: ALL 1024
+    squares in ONE in-place submission (cda_extend_dah_inplace_device) --
+    a 32 GiB EDS arena, so byte offsets run far past 2^32 in every kernel.
+    Submission order is rotated by 512 (position p holds square
+    (p + 512) % 1024), so the squares with full EDS digests (0..127) sit at
+    16-20 GiB.  Every data root and every square's row/column root digest is
+    compared with the oracle fixtures, and a sample of whole EDSs by digest."""
+    import torch
+
+    import bench
+    from celestia_da import testfactory
+    g = _fixture()
+    g["squares"].update(_fixture_rest()["squares"])
+    k, n = 128, 1024
+    W = 2 * k
+    order = [(p + 512) % n for p in range(n)]
+    dev = torch.device("cuda", 0)
+    eds = torch.empty((n, W, W, 512), dtype=torch.uint8, device=dev)
+    for j0, part in testfactory.random_squares(k, order):
+        eds[j0:j0 + part.shape[0], :k, :k] = torch.from_numpy(part).to(dev).view(-1, k, k, 512)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    r, c, dr = rows.cpu().numpy(), cols.cpu().numpy(), roots.cpu().numpy()
+    bad = []
+    for p, i in enumerate(order):
+        want = g["squares"][str(i)]
+        if (dr[p].tobytes().hex() != want["data_root"] or _sha(r[p].reshape(W, 90)) != want["row_roots_sha256"]
+                or _sha(c[p].reshape(W, 90)) != want["col_roots_sha256"]):
+            bad.append((p, i))
+    assert not bad, f"{len(bad)} squares differ from the oracle, first {bad[:4]}"
+    for i in (0, 63, 127):           # at positions 512, 575, 639: offsets 16-20 GiB
+        p = order.index(i)
+        assert _sha(eds[p].cpu().numpy()) == g["squares"][str(i)]["eds_sha256"], (p, i)
+    assert list(bench.shard(0, 1, 1024)) == list(range(1024))
+
+
 def test_shard_partitions_config4():
     import bench
     for world in (1, 2, 4, 8):

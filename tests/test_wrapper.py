@@ -200,3 +200,62 @@ def test_seeded_tree_recomputes_when_fed_other_cells(ctx):
     for c in changed:
         t.push(c)
     assert t.root() == pyref.axis_root(changed, k, 1) != seeded_root
+
+
+@pytest.mark.gpu
+def test_cell_rewritten_in_place_after_extend_shares_gets_recomputed_root(ctx):
+    """a cell rewritten IN PLACE (same backing array) after
+    ExtendShares must not return the extension's stale GPU root -- rsmt2d
+    hashes the cells when RowRoots/ColRoots is first called
+    (pkg/da/data_availability_header.go:44-63 -> computeRoots), so the DAH is
+    that of the rewritten square, and a tree seeded before the rewrite drops
+    its seed."""
+    from celestia_da import da
+    k = 8
+    W = 2 * k
+    ods = testfactory.random_square(k, 21)
+    eds = da.extend_shares(ods)
+    arr = eds.array()
+    seeded_row = eds.row(W - 1)
+    arr[W - 1, W - 2, 100:140] ^= 0x5A            # parity cell of row W-1 / column W-2, in place
+    rows, cols, _ = pyref.dah_from_eds(np.asarray(arr).reshape(W, W, 512).copy())
+    dah = da.new_data_availability_header(eds)
+    assert dah.row_roots == [bytes(r) for r in rows] and dah.column_roots == [bytes(c) for c in cols]
+    assert dah.row_roots[W - 1] == pyref.axis_root([bytes(c) for c in arr[W - 1]], k, W - 1)
+    # a standalone tree seeded with the row as it was, then fed the same
+    # (now rewritten) buffer views, recomputes
+    t = wrapper.new_erasured_namespaced_merkle_tree(k, W - 1, ctx)
+    t.seed(b"\x00" * 90, [np.frombuffer(c, dtype=np.uint8) for c in seeded_row])
+    for c in range(W):
+        t.push(arr[W - 1, c])
+    assert t.root() == dah.row_roots[W - 1]
+
+
+@pytest.mark.gpu
+def test_axis_roots_reports_every_violating_tree(ctx):
+    """cda_nmt_axis_roots' per-tree status must flag EVERY tree
+    that breaks push order, not only the first one (nmt Push
+    ErrInvalidPushOrder per tree; pkg/wrapper/nmt_wrapper.go:93-114)."""
+    k = 8
+    ods = testfactory.random_square(k, 4).reshape(k, k, 512)
+    rows = np.ascontiguousarray(ods[:, :, :].copy())
+    parity = np.zeros((k, k, 512), dtype=np.uint8)
+    cells = np.concatenate([rows, parity], axis=1)          # k trees (rows 0..k-1) of 2k cells
+    bad = (1, 4, 6)
+    for t in bad:                                          # swap two Q0 cells: namespace out of order
+        cells[t, [2, 5]] = cells[t, [5, 2]]
+    n_trees, n_cells, _ = cells.shape
+    out = np.empty((n_trees, 90), dtype=np.uint8)
+    status = np.empty(n_trees, dtype=np.int32)
+    import ctypes as C
+    from celestia_da._lib import CDA_ERR_PUSH_ORDER, ptr
+    axes = np.arange(n_trees, dtype=np.uint32)
+    rc = ctx.lib.cda_nmt_axis_roots(ctx.h, ptr(np.ascontiguousarray(cells)), 512, n_cells, n_trees, k,
+                                    axes.ctypes.data_as(C.POINTER(C.c_uint32)), ptr(out),
+                                    status.ctypes.data_as(C.POINTER(C.c_int32)))
+    assert rc == CDA_ERR_PUSH_ORDER
+    want = [CDA_ERR_PUSH_ORDER if t in bad else 0 for t in range(n_trees)]
+    assert status.tolist() == want
+    for t in range(n_trees):
+        if t not in bad:
+            assert out[t].tobytes() == pyref.axis_root([bytes(c) for c in cells[t]], k, t)
