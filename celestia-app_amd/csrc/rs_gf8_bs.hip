@@ -172,6 +172,11 @@ __device__ __forceinline__ uint32_t swap16(uint32_t v) {   // lane l <- lane l ^
     return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // bit mode: and 0x1F, xor 0x10
 }
 
+// ONE = true (small jobs, e.g. one square: config 2): one codeword per
+// workgroup, lanes 32..63 idle (their loads and stores masked off), so a
+// job of n codewords fills n workgroups instead of n / 2 -- for a single
+// k = 128 square the first launch then covers all 256 CUs instead of 128.
+template <bool ONE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job) {
     rs_err_init(job);
     extern __shared__ uint32_t E[];
@@ -179,10 +184,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     const uint32_t l = threadIdx.x & 63;
     const uint32_t h = (l >> 4) & 1;
     const uint32_t h0 = h ? 0u : 0xFFFFFFFFu;
-    const uint32_t cwg = 2 * blockIdx.x;
+    const uint32_t cwg = ONE ? blockIdx.x : 2 * blockIdx.x;
     const bool s1 = job.n_seg > 1 && cwg >= job.seg[0].n_cw;
     const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
-    const uint32_t c = (s1 ? cwg - job.seg[0].n_cw : cwg) + (l >> 5);
+    const bool live = !ONE || l < 32;
+    const uint32_t c = (s1 ? cwg - job.seg[0].n_cw : cwg) + (ONE ? 0u : (l >> 5));
     const uint32_t col = 16 * (l & 15);
     const uint8_t* src = job.src + blockIdx.y * job.src_sq;
     uint8_t* dst = job.dst + blockIdx.y * job.dst_sq;
@@ -196,12 +202,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint32_t o = s0 + 2 * j * g.src_sh;
-        const uint4 a = *reinterpret_cast<const uint4*>(src + o);
-        const uint4 b = *reinterpret_cast<const uint4*>(src + o + 256);
+        uint4 a = make_uint4(0, 0, 0, 0), b = a;
+        if (live) {
+            a = *reinterpret_cast<const uint4*>(src + o);
+            b = *reinterpret_cast<const uint4*>(src + o + 256);
+        }
         R[8 * j + 0] = a.x; R[8 * j + 1] = a.y; R[8 * j + 2] = a.z; R[8 * j + 3] = a.w;
         R[8 * j + 4] = b.x; R[8 * j + 5] = b.y; R[8 * j + 6] = b.z; R[8 * j + 7] = b.w;
     }
-    if (g.cpy_off != kNoCopy) {
+    if (live && g.cpy_off != kNoCopy) {
         const uint32_t c0 = g.cpy_off + c * g.cpy_cw + col + (16 * u + h) * g.cpy_sh;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -272,8 +281,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     for (int j = 0; j < 8; j++) {
         transpose8(R + 8 * j);
         const uint32_t o = d0 + 2 * j * g.dst_sh;
-        *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * j], R[8 * j + 1], R[8 * j + 2], R[8 * j + 3]);
-        *reinterpret_cast<uint4*>(dst + o + 256) = make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
+        if (live) {
+            *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * j], R[8 * j + 1], R[8 * j + 2], R[8 * j + 3]);
+            *reinterpret_cast<uint4*>(dst + o + 256) =
+                make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
+        }
     }
 }
 
@@ -304,12 +316,25 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
         }();
         static bool attr = false;
         if (lds > 64 * 1024 && !attr) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs8_bs_half_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
+            for (const void* f : {reinterpret_cast<const void*>(rs8_bs_half_kernel<false>),
+                                  reinterpret_cast<const void*>(rs8_bs_half_kernel<true>)}) {
+                hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
             attr = true;
         }
-        hipLaunchKernelGGL(rs8_bs_half_kernel, dim3(ncw / 2, n), dim3(512), lds, s, j);
+        // a job that cannot fill the chip with two codewords per workgroup
+        // (fewer than 2 per CU: one k = 128 square has 256 + 128) takes one
+        // per workgroup (CDA_RS8_ONE=0/1 forces either, A/B knob)
+        static const int one_env = [] {
+            const char* e = getenv("CDA_RS8_ONE");
+            return e ? atoi(e) : -1;
+        }();
+        const bool one = one_env >= 0 ? one_env != 0 : (uint64_t)ncw * n < 2u * 256u;
+        if (one)
+            hipLaunchKernelGGL(rs8_bs_half_kernel<true>, dim3(ncw, n), dim3(512), lds, s, j);
+        else
+            hipLaunchKernelGGL(rs8_bs_half_kernel<false>, dim3(ncw / 2, n), dim3(512), lds, s, j);
         return hipGetLastError();
     }
     const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);

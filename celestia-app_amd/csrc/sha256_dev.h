@@ -417,20 +417,95 @@ CDA_HD void rfc_leaf_u(const uint32_t (&I)[kSlotWords], uint32_t (&D)[8], bool A
     }
     h.digest(A, D);
 }
-// RFC-6962 inner digest sha256(0x01 || a || b) of two digests.
+// ---------------------------------------------------------------------------
+// RFC-6962 inner node, second block.  The 65-B message 0x01 || a || b leaves
+// one data byte in block 1: b[31] || 0x80 || 0 ... || 520 (bits).  Its whole
+// message schedule is a function of that byte, so K[t] + W[t] for all 64
+// rounds is a 64 KiB compile-time table kRfcPadKW[byte][t] and the block runs
+// its rounds with no schedule: 14 instead of ~21.5 VALU ops per round (the
+// chains of the latency-bound data-root levels).
+// ---------------------------------------------------------------------------
+struct RfcPadTable {
+    uint32_t kw[256][64];
+};
+constexpr RfcPadTable make_rfc_pad_table() {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    RfcPadTable t{};
+    for (uint32_t v = 0; v < 256; v++) {
+        uint32_t w[64] = {};
+        w[0] = (v << 24) | 0x00800000u;
+        w[15] = 65u * 8u;
+        for (int i = 16; i < 64; i++) {
+            const uint32_t s0 = crotr(w[i - 15], 7) ^ crotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+            const uint32_t s1 = crotr(w[i - 2], 17) ^ crotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+        }
+        for (int i = 0; i < 64; i++) t.kw[v][i] = K[i] + w[i];
+    }
+    return t;
+}
+#if defined(__HIPCC__)
+__device__ constexpr RfcPadTable kRfcPad = make_rfc_pad_table();
+#endif
+
+// 64 rounds over precomputed K + W words (kw: 16 x uint4 in registers).
+CDA_HD void sha_compress_kw(ShaState& s, const uint4 (&kw)[16]) {
+    uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+    uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        const uint4 q = kw[i / 4];
+        const uint32_t x = (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
+        uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        uint32_t t1 = add3(h, S1, ch(e, f, g)) + x;
+        uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        uint32_t mj = maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = add3(t1, S0, mj);
+    }
+    s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+    s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+CDA_HD void sha_pair_compress_kw(ShaPair& s, const uint4 (&kw)[16], bool A) {
+    const uint32_t r1 = A ? 2u : 6u, r2 = A ? 13u : 11u, r3 = A ? 22u : 25u;
+    uint32_t v0 = s.h[0], v1 = s.h[1], v2 = s.h[2], v3 = s.h[3];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        const uint4 q = kw[i / 4];
+        const uint32_t x = (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
+        const uint32_t S = xor3(__builtin_amdgcn_alignbit(v0, v0, r1), __builtin_amdgcn_alignbit(v0, v0, r2),
+                                __builtin_amdgcn_alignbit(v0, v0, r3));
+        const uint32_t F = pair_sel(ch(v0, v1, v2), maj(v0, v1, v2));
+        const uint32_t Y = pair_sel(v3 + x, 0u);
+        const uint32_t T = add3(S, F, Y);
+        const uint32_t nv = pair_add(T, pair_sel(T, v3));
+        v3 = v2; v2 = v1; v1 = v0; v0 = nv;
+    }
+    s.h[0] += v0; s.h[1] += v1; s.h[2] += v2; s.h[3] += v3;
+}
+
+#if defined(__HIPCC__)
+// RFC-6962 inner digest sha256(0x01 || a || b) of two digests; block 1 from
+// kRfcPad (its 256 B row, loaded before block 0 runs).
 template <bool PAIR>
 CDA_HD void rfc_inner_u(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&D)[8], bool A) {
     Sha<PAIR> h;
     h.init(A);
+    const uint4* row = reinterpret_cast<const uint4*>(kRfcPad.kw[b[7] & 0xFFu]);
+    uint4 kw[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) kw[q] = row[q];
     uint32_t w[16];
 #pragma unroll
-    for (int blk = 0; blk < 2; blk++) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(a, b, 16 * blk + j);
-        h.compress(w, A);
-    }
+    for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(a, b, j);
+    h.compress(w, A);
+    if constexpr (PAIR)
+        sha_pair_compress_kw(h.st, kw, A);
+    else
+        sha_compress_kw(h.st, kw);
     h.digest(A, D);
 }
+#endif
 
 // NMT HashNode of two child slots (big-endian words) into a parent slot
 // (little-endian words), per thread or per lane pair; no mid-state branch
