@@ -270,7 +270,7 @@ class Engine {
     hipStream_t aux_stream_ = nullptr;
     std::vector<hipEvent_t> sync_events_;
     uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
-    uint32_t hash_split_ = 2;       // CDA_HASH_SPLIT: hash the batch in this many parts on as many streams (0/1 = off)
+    int hash_split_ = -1;           // CDA_HASH_SPLIT: hash the batch in this many parts on as many streams (0/1 = off, -1 = auto)
     static constexpr uint32_t kMaxHashParts = 4;
     uint32_t host_chunk_ = 4;       // CDA_HOST_CHUNK: squares per H2D/RS/D2H chunk of a host-buffer batch
     bool host_full_d2h_ = false;    // CDA_HOST_FULL_D2H: EDS back as one contiguous copy (no host Q0 copy)

@@ -166,7 +166,7 @@ int Engine::init() {
         return rc;
     }
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
-    if (const char* env = getenv("CDA_HASH_SPLIT")) hash_split_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_HASH_SPLIT")) hash_split_ = atoi(env);
     if (const char* env = getenv("CDA_HOST_CHUNK")) host_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
@@ -487,7 +487,12 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     // profiles/r02_hash_split.txt).  CDA_HASH_SPLIT=0 turns it off; stage
     // profiling (bench's separate stage pass) uses the one-stream schedule so
     // every stage's events time its own kernels.
-    const uint32_t parts = std::min<uint32_t>(std::min<uint32_t>(hash_split_, n), kMaxHashParts);
+    // auto: two parts up to 256 squares (+0.3-1.8 % at 128, profiles/r02_hash_split.txt), one above --
+    // at config 4's 1024 squares per launch the level tails no longer matter (21 465 split vs 21 528
+    // one stream, profiles/r03a/bench_split0.json), and one stream keeps every launch of a kernel the
+    // same shape, so per-launch profiler counters divide by a known square count
+    const uint32_t want = hash_split_ >= 0 ? (uint32_t)hash_split_ : (n <= 256 ? 2u : 1u);
+    const uint32_t parts = std::min<uint32_t>(std::min<uint32_t>(want, n), kMaxHashParts);
     if (parts > 1 && !profiling_) {
         hipEvent_t go = sync_event(0);
         if (!go || !sync_event(parts)) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");

@@ -323,8 +323,14 @@ constexpr uint32_t kTopThreads = 128;   // parents per workgroup: tpw = 256 / n_
 
 template <bool PAIR>
 __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top_kernel(
-    const Forest2 fs, uint32_t n_in, uint32_t tpw, uint32_t* __restrict__ dig, uint32_t n_dig, uint32_t rfc_levels) {
+    const Forest2 fs, uint32_t n_in, uint32_t tpw, uint32_t* __restrict__ dig, uint32_t n_dig, uint32_t rfc_levels,
+    uint32_t helpers) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][kTopThreads][kSlotWords];
+    // schedule helpers (PAIR, levels of <= 64 parents): K + W of blocks 1 and
+    // 2 of unit u's node at kwb[u][block - 1][t] (rows padded 4 words so the
+    // units' 16-B reads spread over the banks)
+    constexpr uint32_t kKwRow = 2 * 64 + 4;
+    __shared__ __attribute__((aligned(16))) uint32_t kwb[PAIR ? 64 : 1][kKwRow];
     const size_t sq = blockIdx.y;
     const uint32_t n_trees = fs.f[0].n_trees + fs.f[1].n_trees;
     const uint32_t u = PAIR ? threadIdx.x >> 1 : threadIdx.x;   // unit (parent) index
@@ -336,7 +342,61 @@ __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top
         const uint32_t half = m / 2;
         const uint32_t j = u / half, p = u % half;   // tree j of this workgroup, parent p
         const uint32_t g = blockIdx.x * tpw + j;
-        if (j < tpw && g < n_trees) {
+        if (PAIR && helpers && m < n_in && tpw * half <= 64) {
+            // At most two waves of parents: waves 2 and 3 would idle, so they
+            // compute the message schedules of blocks 1 and 2 of every node
+            // (one lane per block) while waves 0-1 run block 0; the parents'
+            // lane pairs then run blocks 1 and 2 rounds-only (sha_pair_compress_kw:
+            // the chain of dependent compressions is the critical wave's
+            // instruction count).
+            Sha<true> h;
+            const bool work = threadIdx.x < 128 && j < tpw && g < n_trees;
+            uint32_t L[kSlotWords], R[kSlotWords];
+            if (threadIdx.x >= 128) {
+                const uint32_t hi = threadIdx.x - 128, hu = hi >> 1, hb = 1 + (hi & 1);
+                const uint32_t hj = hu / half, hp = hu % half;
+                if (hj < tpw && blockIdx.x * tpw + hj < n_trees) {
+#pragma unroll
+                    for (int i = 0; i < kSlotWords; i++) {
+                        L[i] = bswap32(buf[cur][hj * m + 2 * hp][i]);
+                        R[i] = bswap32(buf[cur][hj * m + 2 * hp + 1][i]);
+                    }
+                    uint32_t w[16];
+#pragma unroll
+                    for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * hb + i);
+                    sha_schedule_kw(w, &kwb[hu][64 * (hb - 1)]);
+                }
+            } else if (work) {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) {
+                    L[i] = bswap32(buf[cur][j * m + 2 * p][i]);
+                    R[i] = bswap32(buf[cur][j * m + 2 * p + 1][i]);
+                }
+                h.init(A);
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, i);
+                h.compress(w, A);
+            }
+            __syncthreads();   // the helpers' schedules are in kwb
+            if (work) {
+#pragma unroll
+                for (int b = 0; b < 2; b++) {
+                    uint4 kw[16];
+                    const uint4* row = reinterpret_cast<const uint4*>(&kwb[u][64 * b]);
+#pragma unroll
+                    for (int q = 0; q < 16; q++) kw[q] = row[q];
+                    sha_pair_compress_kw(h.st, kw, A);
+                }
+                uint32_t D[8];
+                h.digest(A, D);
+                inner_node_words(L, R, D, o);
+                if (m > 2 && writer) {
+#pragma unroll
+                    for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][u][i] = o[i];
+                }
+            }
+        } else if (j < tpw && g < n_trees) {
             uint32_t L[kSlotWords], R[kSlotWords];
             if (m == n_in) {
                 const bool f1 = g >= fs.f[0].n_trees;
@@ -678,10 +738,16 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
     const uint64_t parents = (uint64_t)n * trees * (n_in / 2);
     const bool pair = pair_sha_enabled() && 2 * parents <= 65536;
     const dim3 grid((trees + tpw - 1) / tpw, n);
+    // CDA_TOP_HELPERS=0 (A/B knob): no schedule-helper waves in the narrow levels
+    static const uint32_t helpers = [] {
+        const char* e = getenv("CDA_TOP_HELPERS");
+        return e && atoi(e) == 0 ? 0u : 1u;
+    }();
     if (pair)
-        hipLaunchKernelGGL(tree_top_kernel<true>, grid, dim3(2 * kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv);
+        hipLaunchKernelGGL(tree_top_kernel<true>, grid, dim3(2 * kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv,
+                           helpers);
     else
-        hipLaunchKernelGGL(tree_top_kernel<false>, grid, dim3(kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv);
+        hipLaunchKernelGGL(tree_top_kernel<false>, grid, dim3(kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv, 0u);
     return hipGetLastError();
 }
 

@@ -484,6 +484,34 @@ CDA_HD void sha_pair_compress_kw(ShaPair& s, const uint4 (&kw)[16], bool A) {
     s.h[0] += v0; s.h[1] += v1; s.h[2] += v2; s.h[3] += v3;
 }
 
+// K[t] + W[t] of all 64 rounds of one block (w: its 16 message words,
+// consumed) into kw (64 words, 16-B aligned; e.g. LDS): the message schedule
+// computed by a helper lane for sha_*_compress_kw on another wave.
+CDA_HD void sha_schedule_kw(uint32_t (&w)[16], uint32_t* kw) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    uint4* q = reinterpret_cast<uint4*>(kw);
+#pragma unroll
+    for (int i = 0; i < 64; i += 4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int t = i + r;
+            uint32_t wi;
+            if (t < 16) {
+                wi = w[t];
+            } else {
+                const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                wi = add3(w[t & 15], s0, w[(t - 7) & 15]) + s1;
+                w[t & 15] = wi;
+            }
+            v[r] = K[t] + wi;
+        }
+        q[i / 4] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 #if defined(__HIPCC__)
 // RFC-6962 inner digest sha256(0x01 || a || b) of two digests; block 1 from
 // kRfcPad (its 256 B row, loaded before block 0 runs).

@@ -7,7 +7,7 @@ the per-dispatch means of every counter of the separate --pmc passes, HBM
 bytes per launch with MI355X_MICROARCH.md's gfx950 correction (FETCH_SIZE
 counts half the bytes of a wide coalesced streaming read: x2; WRITE_SIZE
 exact; both reported in KiB), and -- because the run has a fixed shape
-(CDA_HASH_SPLIT=0, one batch size) -- the per-step and per-square figures:
+(one batch size, one hash stream) -- the per-step and per-square figures:
 
   launches_per_step_k<K>    = launches / steps_total
   hbm_bytes_per_square_k<K> = hbm_bytes_per_launch x launches_per_step / squares_per_step
@@ -42,7 +42,7 @@ def main(src, dst, k, steps_total, squares, command):
     out = json.load(open(dst)) if os.path.exists(dst) else {}
     cfg = out.setdefault("_config", {})
     cfg[f"k{k}"] = {"k": k, "steps_total": steps_total, "squares_per_step": squares, "command": command,
-                    "note": "fixed launch shape: CDA_HASH_SPLIT=0, one batch size; counters are per-dispatch "
+                    "note": "fixed launch shape: one batch size, one hash stream; counters are per-dispatch "
                             "means of separate --pmc passes"}
     cur = collections.defaultdict(dict)
     for row in csv.DictReader(open(f"{src}/trace/run_kernel_stats.csv")):

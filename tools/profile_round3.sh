@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 evidence in one GPU call (run via gpurun), fixed launch shapes so
 # every per-launch counter divides by a known square count:
-#   k = 128: config 4's 1024 squares per step (bench default), CDA_HASH_SPLIT=0
+#   k = 128: config 4's 1024 squares per step (bench default: one hash stream)
 #   k = 512: one square per step (config 3)
 # kernel trace + stats, then separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ
 # issue counters; SQ wait counters), summarised by tools/pmc_summary3.py into
@@ -11,7 +11,7 @@ TAG=${1:-r03}
 R=$GRAFT_REPO_ROOT
 cd /tmp
 export TMPDIR=/tmp
-export CDA_HASH_SPLIT=0
+
 SUM=$R/gpurun_out/${TAG}_pmc.json
 rm -f $SUM
 for K in 128 512; do
@@ -27,7 +27,7 @@ for K in 128 512; do
   timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $B > $OUT/write.log 2>&1 || exit 3
   timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 $B > $OUT/sq.log 2>&1 || exit 4
   timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/wait -o run -- python3 $B > $OUT/wait.log 2>&1 || exit 5
-  cd $R && python3 tools/pmc_summary3.py $OUT $SUM $K $STEPS $SQ "CDA_HASH_SPLIT=0 python3 ${B#$R/}" > $OUT/pmc_summary.log 2>&1 || exit 6
+  cd $R && python3 tools/pmc_summary3.py $OUT $SUM $K $STEPS $SQ "python3 ${B#$R/}" > $OUT/pmc_summary.log 2>&1 || exit 6
   cp $OUT/trace/run_kernel_stats.csv $R/gpurun_out/${TAG}_k${K}_kernel_stats.csv
   cd /tmp
 done
