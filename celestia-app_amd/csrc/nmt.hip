@@ -19,6 +19,7 @@
 // leaf / per parent node; each NMT level of all 4k trees of every square in
 // the batch is one launch.  SHA-256 is pure 32-bit VALU work (no MFMA).
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "cda_kernels.h"
@@ -361,9 +362,17 @@ __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top
                         L[i] = bswap32(buf[cur][hj * m + 2 * hp][i]);
                         R[i] = bswap32(buf[cur][hj * m + 2 * hp + 1][i]);
                     }
+                    // the block index must be a compile-time constant in
+                    // node_msg (a run-time one indexes L / R dynamically:
+                    // private memory)
                     uint32_t w[16];
+                    if (hb == 1) {
 #pragma unroll
-                    for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 * hb + i);
+                        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 + i);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 32 + i);
+                    }
                     sha_schedule_kw(w, &kwb[hu][64 * (hb - 1)]);
                 }
             } else if (work) {
@@ -573,11 +582,145 @@ __device__ __forceinline__ void data_root_level(const uint32_t* __restrict__ in,
 
 constexpr uint32_t kPairMaxParents = 128;   // 256 lanes: one wave per SIMD of the CU
 
-__global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
+// 16 rounds [R0, R0 + 16) of a lane-pair compression over precomputed
+// K + W words (v: the pair's 4 state words, as in sha_pair_compress).
+template <int R0>
+__device__ __forceinline__ void pair_rounds16(uint32_t (&v)[4], const uint32_t (&kw)[16], bool A) {
+    const uint32_t r1 = A ? 2u : 6u, r2 = A ? 13u : 11u, r3 = A ? 22u : 25u;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t S = xor3(__builtin_amdgcn_alignbit(v[0], v[0], r1), __builtin_amdgcn_alignbit(v[0], v[0], r2),
+                                __builtin_amdgcn_alignbit(v[0], v[0], r3));
+        const uint32_t F = pair_sel(ch(v[0], v[1], v[2]), maj(v[0], v[1], v[2]));
+        const uint32_t Y = pair_sel(v[3] + kw[i], 0u);
+        const uint32_t T = add3(S, F, Y);
+        const uint32_t nv = pair_add(T, pair_sel(T, v[3]));
+        v[3] = v[2]; v[2] = v[1]; v[1] = v[0]; v[0] = nv;
+    }
+}
+
+// Schedule words [T0, T0 + 16) (T0 >= 16) of one block into kw[T0 .. T0+16)
+// as K + W (w: the 16-word ring, updated in place).
+template <int T0>
+__device__ __forceinline__ void schedule16_kw(uint32_t (&w)[16], uint32_t* kw) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    uint4* q = reinterpret_cast<uint4*>(kw + T0);
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int t = T0 + i + r;
+            const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            const uint32_t wi = add3(w[t & 15], s0, w[(t - 7) & 15]) + s1;
+            w[t & 15] = wi;
+            v[r] = K[t] + wi;
+        }
+        q[i / 4] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// One data-root level of m <= 32 parents with schedule helpers: wave 0 holds
+// the parents' lane pairs, and one lane of waves 1.. per parent computes the
+// message schedule of its block 0 (16 words at a time, through LDS, one
+// barrier per 16 rounds) while the pair runs the rounds; block 1 comes from
+// kRfcPad.  The pair's chain then carries no schedule work at all (DESIGN.md
+// 3.5: the chain costs its wave's instruction count).  Every thread of the
+// workgroup must call this (it holds barriers).
+constexpr uint32_t kDrKwRow = 68;   // 64 words + 4 of padding (bank spread)
+__device__ __forceinline__ void data_root_level_helped(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       uint32_t m, uint32_t (*kwb)[kDrKwRow]) {
+    constexpr uint32_t K[64] = CDA_SHA_K;
+    const bool A = threadIdx.x & 1;
+    const uint32_t i = threadIdx.x / 2, hi = threadIdx.x - 64;
+    const bool rounds = threadIdx.x < 64 && i < m;
+    const bool helper = threadIdx.x >= 64 && hi < m;
+    const uint32_t p = rounds ? i : hi;
+    uint32_t a[8], b[8], w[16];
+    if (rounds || helper) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[j] = in[(2 * p) * 8 + j];
+            b[j] = in[(2 * p + 1) * 8 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(a, b, j);
+    }
+    ShaPair st;
+    sha_pair_init(st, A);
+    uint32_t v[4] = {st.h[0], st.h[1], st.h[2], st.h[3]};
+    uint32_t kw[16];
+    // block 1's K + W row (kRfcPad), streamed 16 words at a time
+    const uint4* row = reinterpret_cast<const uint4*>(kRfcPad.kw[(rounds ? b[7] : 0u) & 0xFFu]);
+    uint4 nx[4];
+    if (rounds) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) kw[t] = K[t] + w[t];
+        pair_rounds16<0>(v, kw, A);
+    } else if (helper) {
+        schedule16_kw<16>(w, kwb[hi]);
+    }
+    __syncthreads();
+    auto phase = [&](auto R0c) {
+        constexpr int R0 = decltype(R0c)::value;
+        if (rounds) {
+            const uint4* q = reinterpret_cast<const uint4*>(&kwb[i][R0]);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const uint4 x = q[c];
+                kw[4 * c] = x.x; kw[4 * c + 1] = x.y; kw[4 * c + 2] = x.z; kw[4 * c + 3] = x.w;
+            }
+            pair_rounds16<R0>(v, kw, A);
+        } else if (helper && R0 + 16 < 64) {
+            schedule16_kw<(R0 + 16 < 64 ? R0 + 16 : 48)>(w, kwb[hi]);
+        }
+    };
+    phase(std::integral_constant<int, 16>{});
+    __syncthreads();
+    phase(std::integral_constant<int, 32>{});
+    __syncthreads();
+    if (rounds) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) nx[c] = row[c];   // in flight during rounds 48..63
+    }
+    phase(std::integral_constant<int, 48>{});
+    if (rounds) {
+        st.h[0] += v[0]; st.h[1] += v[1]; st.h[2] += v[2]; st.h[3] += v[3];
+        v[0] = st.h[0]; v[1] = st.h[1]; v[2] = st.h[2]; v[3] = st.h[3];
+        auto block1 = [&](auto Cc) {
+            constexpr int C = decltype(Cc)::value;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                kw[4 * c] = nx[c].x; kw[4 * c + 1] = nx[c].y; kw[4 * c + 2] = nx[c].z; kw[4 * c + 3] = nx[c].w;
+            }
+            if constexpr (C < 3) {
+#pragma unroll
+                for (int c = 0; c < 4; c++) nx[c] = row[4 * (C + 1) + c];
+            }
+            pair_rounds16<16 * C>(v, kw, A);
+        };
+        block1(std::integral_constant<int, 0>{});
+        block1(std::integral_constant<int, 1>{});
+        block1(std::integral_constant<int, 2>{});
+        block1(std::integral_constant<int, 3>{});
+        st.h[0] += v[0]; st.h[1] += v[1]; st.h[2] += v[2]; st.h[3] += v[3];
+        uint32_t D[8];
+        sha_pair_digest(st, A, D);
+        if (!A) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) out[i * 8 + j] = D[j];
+        }
+    }
+}
+
+__global__ __launch_bounds__(512) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
                                                                uint8_t* __restrict__ data_roots,
                                                                const uint32_t* __restrict__ err,
                                                                int32_t* __restrict__ status, uint32_t pair_ok) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [n/2][8] | [n/4][8]
+    __shared__ __attribute__((aligned(16))) uint32_t kwb[32][kDrKwRow];   // schedule helpers' K + W
     const size_t sq = blockIdx.x;
     const uint32_t* D = dig + sq * (size_t)n * 8;
     uint32_t* src = hs;
@@ -585,7 +728,9 @@ __global__ __launch_bounds__(1024) void data_root_digest_kernel(const uint32_t* 
     for (uint32_t m = n / 2; m >= 1; m >>= 1) {
         const uint32_t* in = m == n / 2 ? D : src;
         uint32_t* out = m == n / 2 ? src : dst;
-        if (pair_ok && m <= kPairMaxParents && 2 * m <= blockDim.x)
+        if (pair_ok == 2 && m <= 32 && blockDim.x >= 128)
+            data_root_level_helped(in, out, m, kwb);
+        else if (pair_ok && m <= kPairMaxParents && 2 * m <= blockDim.x)
             data_root_level<true>(in, out, m);
         else
             data_root_level<false>(in, out, m);
@@ -790,12 +935,19 @@ hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint3
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    // a thread per first-level parent (<= 1024), and room for the lane pairs
-    uint32_t threads = std::min<uint32_t>(n_items / 2, 1024);
+    // a thread per first-level parent (<= 512: more would cap the kernel at
+    // 128 VGPRs and spill the helpers' registers), and room for the lane pairs
+    uint32_t threads = std::min<uint32_t>(n_items / 2, 512);
     threads = std::max<uint32_t>(threads, std::min<uint32_t>(n_items, 2 * kPairMaxParents));
     threads = std::max<uint32_t>((threads + 63) / 64 * 64, 64);
+    // CDA_DR_HELPERS=0 (A/B knob): no schedule helpers in the narrow data-root levels
+    static const bool dr_helpers = [] {
+        const char* e = getenv("CDA_DR_HELPERS");
+        return !(e && atoi(e) == 0);
+    }();
+    const uint32_t mode = pair_sha_enabled() ? (dr_helpers ? 2u : 1u) : 0u;
     hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots,
-                       status ? err : nullptr, status, pair_sha_enabled() ? 1u : 0u);
+                       status ? err : nullptr, status, mode);
     return hipGetLastError();
 }
 

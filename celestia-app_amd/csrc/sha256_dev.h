@@ -514,7 +514,8 @@ CDA_HD void sha_schedule_kw(uint32_t (&w)[16], uint32_t* kw) {
 
 #if defined(__HIPCC__)
 // RFC-6962 inner digest sha256(0x01 || a || b) of two digests; block 1 from
-// kRfcPad (its 256 B row, loaded before block 0 runs).
+// kRfcPad (its 256 B row: the first 64 B are loaded before block 0 runs, the
+// rest 16 rounds ahead of use, so at most 32 table words are live).
 template <bool PAIR>
 CDA_HD void rfc_inner_u(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t (&D)[8], bool A) {
     Sha<PAIR> h;
@@ -522,11 +523,13 @@ CDA_HD void rfc_inner_u(const uint32_t (&a)[8], const uint32_t (&b)[8], uint32_t
     const uint4* row = reinterpret_cast<const uint4*>(kRfcPad.kw[b[7] & 0xFFu]);
     uint4 kw[16];
 #pragma unroll
-    for (int q = 0; q < 16; q++) kw[q] = row[q];
+    for (int q = 0; q < 4; q++) kw[q] = row[q];
     uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(a, b, j);
     h.compress(w, A);
+#pragma unroll
+    for (int q = 4; q < 16; q++) kw[q] = row[q];
     if constexpr (PAIR)
         sha_pair_compress_kw(h.st, kw, A);
     else
