@@ -211,11 +211,22 @@ __device__ __forceinline__ TabRegs load_tabs(const uint32_t* p) {
     r.a = sload16(p);
     return r;
 }
+// CDA_RS16_LDS_A=1 (experiment): passes A / A' read both table halves of
+// every constant from LDS (20-dword records: src0 dwords 0..11, src1 12..19)
+// instead of a scalar load per group, and the exchanges move lo and hi
+// registers in separate 64 KiB rounds to make room.  Scalar loads return out
+// of order, so the SMEM form cannot prefetch deeper than one group; LDS reads
+// are in order and never miss.
+#ifndef CDA_RS16_LDS_A
+#define CDA_RS16_LDS_A 0
+#endif
+constexpr uint32_t kTbStride = CDA_RS16_LDS_A ? 20 : 8;   // dwords per constant in the LDS table
+constexpr uint32_t kTbSrc1 = CDA_RS16_LDS_A ? 12 : 0;     // offset of the src1 halves in a record
 struct TabB {   // src1 halves of one constant, [a][lo/hi] as 8 dwords
     uint4 b0, b1;
 };
 __device__ __forceinline__ TabB load_tab_b(const uint32_t* TB, uint32_t idx) {
-    const uint4* p = reinterpret_cast<const uint4*>(TB + idx * 8);
+    const uint4* p = reinterpret_cast<const uint4*>(TB + idx * kTbStride + kTbSrc1);
     return TabB{p[0], p[1]};
 }
 
@@ -355,6 +366,39 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
         }
     });
 }
+// Passes A / A' with every table dword from LDS (CDA_RS16_LDS_A): per group
+// five 16-B reads of the constant's record at TB (+ lidxf(g, d) records), no
+// scalar loads; the compiler schedules the reads (in order, LDS-latency).
+template <int N, bool INV, bool DFS, class LIdxF, class Fin = NoFin>
+__device__ __forceinline__ void layers_regs_lds(uint32_t (&lo)[N], uint32_t (&hi)[N], const uint32_t* TB,
+                                                LIdxF lidxf, Fin fin = Fin{}) {
+    constexpr int NG = N - 1;
+    sfor<0, NG, 1>([&](auto II) {
+        constexpr int I = decltype(II)::value;
+        constexpr int g = grp_at<N, INV, DFS>(I, false), d = grp_at<N, INV, DFS>(I, true);
+        const uint4* p = reinterpret_cast<const uint4*>(TB + lidxf(g, d) * kTbStride);
+        const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+        const uint32_t t[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+        const uint32_t bv[8] = {q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w};
+        sfor<g, g + d, 1>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            if constexpr (INV) {
+                hi[i + d] ^= hi[i];
+                lo[i + d] ^= lo[i];
+                mul_add16_c3(lo[i], hi[i], lo[i + d], hi[i + d], t, bv);
+            } else {
+                mul_add16_c3(lo[i], hi[i], lo[i + d], hi[i + d], t, bv);
+                lo[i + d] ^= lo[i];
+                hi[i + d] ^= hi[i];
+            }
+        });
+        if constexpr (!INV && d == 1) {
+            fin(std::integral_constant<int, g>{});
+            fin(std::integral_constant<int, g + 1>{});
+        }
+    });
+}
+
 #ifndef CDA_RS16_DFS
 #define CDA_RS16_DFS 1
 #endif
@@ -362,22 +406,30 @@ constexpr bool kRs16Dfs = CDA_RS16_DFS != 0;
 template <int N, class IdxF, class LIdxF>
 __device__ __forceinline__ void ifft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
                                           IdxF idxf, LIdxF lidxf) {
-    layers_regs<N, true, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, NoFin{}, lidxf);
+    if constexpr (CDA_RS16_LDS_A)
+        layers_regs_lds<N, true, kRs16Dfs>(lo, hi, TB, lidxf);
+    else
+        layers_regs<N, true, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, NoFin{}, lidxf);
 }
 template <int N, class IdxF, class Fin, class LIdxF>
 __device__ __forceinline__ void fft_regs(uint32_t (&lo)[N], uint32_t (&hi)[N], const Tab16& T, const uint32_t* TB,
                                          IdxF idxf, Fin fin, LIdxF lidxf) {
-    layers_regs<N, false, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, fin, lidxf);
+    if constexpr (CDA_RS16_LDS_A)
+        layers_regs_lds<N, false, kRs16Dfs>(lo, hi, TB, lidxf, fin);
+    else
+        layers_regs<N, false, false, 1, kRs16Dfs>(lo, hi, T, TB, idxf, fin, lidxf);
 }
 
-constexpr uint32_t kXchgBytes = 16 * 16 * 2 * 64 * 4;   // [src wave][dst wave][lo/hi][lane] dwords
+// exchange buffer: [src wave][dst wave][lo/hi][lane] dwords (LDS_A: lo and
+// hi in separate rounds, [src][dst][lane])
+constexpr uint32_t kXchgBytes = 16 * 16 * (CDA_RS16_LDS_A ? 1 : 2) * 64 * 4;
 // + the src1 table halves of the 2K-1 constants, 32 B each (K = 512: 160 KiB total)
 template <int K>
 constexpr uint32_t cw_lds_bytes() {
 #ifdef CDA_RS16_CHUNK2
     return kXchgBytes;
 #else
-    return kXchgBytes + (2 * K - 1) * 32;
+    return kXchgBytes + (2 * K - 1) * kTbStride * 4;
 #endif
 }
 
@@ -403,10 +455,17 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     {   // stage dwords 12..19 of every constant's record (its src1 halves)
         uint32_t* tb = X + kXchgBytes / 4;
         for (uint32_t i = threadIdx.x; i < 2 * K - 1; i += 1024) {
-            const uint4* src = reinterpret_cast<const uint4*>(tab + (size_t)i * kGf16TabWords + 12);
-            uint4* dst = reinterpret_cast<uint4*>(tb + i * 8);
-            dst[0] = src[0];
-            dst[1] = src[1];
+            if constexpr (CDA_RS16_LDS_A) {   // the whole record: dwords 0..19
+                const uint4* src = reinterpret_cast<const uint4*>(tab + (size_t)i * kGf16TabWords);
+                uint4* dst = reinterpret_cast<uint4*>(tb + i * kTbStride);
+#pragma unroll
+                for (int q = 0; q < 5; q++) dst[q] = src[q];
+            } else {
+                const uint4* src = reinterpret_cast<const uint4*>(tab + (size_t)i * kGf16TabWords + 12);
+                uint4* dst = reinterpret_cast<uint4*>(tb + i * 8);
+                dst[0] = src[0];
+                dst[1] = src[1];
+            }
         }
         __syncthreads();
     }
@@ -449,37 +508,46 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     // residue q lives in registers {R*t + q}.
     uint32_t lo[S], hi[S];
     auto xbar = [] { __syncthreads(); };
+    // CDA_RS16_LDS_A: the lo and hi registers of a round move in two
+    // sub-rounds through a 64 KiB buffer ([src][dst][lane])
+    constexpr int NH = CDA_RS16_LDS_A ? 2 : 1;   // sub-rounds per round
+    auto xw = [&](uint32_t src_w, uint32_t dst_w, int h) -> uint32_t& {
+        if constexpr (CDA_RS16_LDS_A)
+            return X[(src_w * 16 + dst_w) * 64 + lane];
+        else
+            return X[((src_w * 16 + dst_w) * 2 + h) * 64 + lane];
+    };
     auto xchg_a_to_b = [&]() {
-        sfor<0, R, 1>([&](auto qq) {
-            constexpr int q = decltype(qq)::value;
-            if (q) xbar();
+        sfor<0, R * NH, 1>([&](auto qh) {
+            constexpr int q = decltype(qh)::value / NH, hh = decltype(qh)::value % NH;
+            if (decltype(qh)::value) xbar();
             sfor<0, 16, 1>([&](auto jj) {
                 constexpr int j = R * decltype(jj)::value + q;
-                X[((wave * 16 + jj.value) * 2 + 0) * 64 + lane] = lo[j];
-                X[((wave * 16 + jj.value) * 2 + 1) * 64 + lane] = hi[j];
+                if (NH == 1 || hh == 0) xw(wave, jj.value, 0) = lo[j];
+                if (NH == 1 || hh == 1) xw(wave, jj.value, 1) = hi[j];
             });
             xbar();
             sfor<0, 16, 1>([&](auto tt) {
                 constexpr int j = R * decltype(tt)::value + q;
-                lo[j] = X[((tt.value * 16 + wave) * 2 + 0) * 64 + lane];
-                hi[j] = X[((tt.value * 16 + wave) * 2 + 1) * 64 + lane];
+                if (NH == 1 || hh == 0) lo[j] = xw(tt.value, wave, 0);
+                if (NH == 1 || hh == 1) hi[j] = xw(tt.value, wave, 1);
             });
         });
     };
     auto xchg_b_to_a = [&]() {
-        sfor<0, R, 1>([&](auto qq) {
-            constexpr int q = decltype(qq)::value;
+        sfor<0, R * NH, 1>([&](auto qh) {
+            constexpr int q = decltype(qh)::value / NH, hh = decltype(qh)::value % NH;
             xbar();
             sfor<0, 16, 1>([&](auto tt) {
                 constexpr int j = R * decltype(tt)::value + q;
-                X[((tt.value * 16 + wave) * 2 + 0) * 64 + lane] = lo[j];
-                X[((tt.value * 16 + wave) * 2 + 1) * 64 + lane] = hi[j];
+                if (NH == 1 || hh == 0) xw(tt.value, wave, 0) = lo[j];
+                if (NH == 1 || hh == 1) xw(tt.value, wave, 1) = hi[j];
             });
             xbar();
             sfor<0, 16, 1>([&](auto jj) {
                 constexpr int j = R * decltype(jj)::value + q;
-                lo[j] = X[((wave * 16 + jj.value) * 2 + 0) * 64 + lane];
-                hi[j] = X[((wave * 16 + jj.value) * 2 + 1) * 64 + lane];
+                if (NH == 1 || hh == 0) lo[j] = xw(wave, jj.value, 0);
+                if (NH == 1 || hh == 1) hi[j] = xw(wave, jj.value, 1);
             });
         });
     };
@@ -497,7 +565,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
         asm volatile("" : "+s"(b));
         return b;
     };
-    ifft_regs<S>(lo, hi, T, TB + 8 * S * wave, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); },
+    ifft_regs<S>(lo, hi, T, TB + kTbStride * S * wave, [&](int g, int d) { return (uint32_t)(K - 1 + g + d) + wave_base(); },
                      [](int g, int d) { return (uint32_t)(K - 1 + g + d); });
     xchg_a_to_b();
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
@@ -528,7 +596,7 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
     // parity shard j is stored as soon as its last butterfly is done
     auto store_j = [&](auto jj) { st(E, d0 + (base + jj.value) * ds, lo[jj.value], hi[jj.value]); };
-    fft_regs<S>(lo, hi, T, TB + 8 * S * wave, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); },
+    fft_regs<S>(lo, hi, T, TB + kTbStride * S * wave, [&](int g, int d) { return (uint32_t)(g + d - 1) + wave_base(); },
                 store_j, [](int g, int d) { return (uint32_t)(g + d - 1); });
 }
 
