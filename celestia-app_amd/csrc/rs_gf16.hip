@@ -211,14 +211,19 @@ __device__ __forceinline__ TabRegs load_tabs(const uint32_t* p) {
     r.a = sload16(p);
     return r;
 }
-// CDA_RS16_LDS_A=1 (experiment): passes A / A' read both table halves of
-// every constant from LDS (20-dword records: src0 dwords 0..11, src1 12..19)
-// instead of a scalar load per group, and the exchanges move lo and hi
-// registers in separate 64 KiB rounds to make room.  Scalar loads return out
-// of order, so the SMEM form cannot prefetch deeper than one group; LDS reads
-// are in order and never miss.
+// Passes A / A' read both table halves of every constant from LDS (20-dword
+// records: src0 dwords 0..11, src1 12..19) instead of a scalar load per
+// group, and the exchanges move lo and hi registers in separate 64 KiB rounds
+// to make room (128 + 80 KiB would not fit).  The per-wave constants of those
+// passes (16 waves x 31 groups x 96 B) do not fit the scalar cache, so every
+// scalar load was an L2 round trip, and scalar loads return out of order, so
+// they could not be prefetched deeper than one group: all waves of a SIMD
+// waited together (round 2).  LDS reads are in order, never
+// miss, and the compiler schedules them ahead.  Measured -54 us per k = 512
+// square (1.218 -> 1.162 ms, profiles/r03c/ldsa_ab.txt).  CDA_RS16_LDS_A=0
+// builds the round-2 scalar-load form (A/B).
 #ifndef CDA_RS16_LDS_A
-#define CDA_RS16_LDS_A 0
+#define CDA_RS16_LDS_A 1
 #endif
 constexpr uint32_t kTbStride = CDA_RS16_LDS_A ? 20 : 8;   // dwords per constant in the LDS table
 constexpr uint32_t kTbSrc1 = CDA_RS16_LDS_A ? 12 : 0;     // offset of the src1 halves in a record
