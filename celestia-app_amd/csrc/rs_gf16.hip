@@ -225,6 +225,10 @@ __device__ __forceinline__ TabRegs load_tabs(const uint32_t* p) {
 #ifndef CDA_RS16_LDS_A
 #define CDA_RS16_LDS_A 1
 #endif
+// CDA_RS16_LDS_B=1 (experiment, needs LDS_A): pass B's tables from LDS as well
+#ifndef CDA_RS16_LDS_B
+#define CDA_RS16_LDS_B 0
+#endif
 constexpr uint32_t kTbStride = CDA_RS16_LDS_A ? 20 : 8;   // dwords per constant in the LDS table
 constexpr uint32_t kTbSrc1 = CDA_RS16_LDS_A ? 12 : 0;     // offset of the src1 halves in a record
 struct TabB {   // src1 halves of one constant, [a][lo/hi] as 8 dwords
@@ -374,30 +378,42 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
 // Passes A / A' with every table dword from LDS (CDA_RS16_LDS_A): per group
 // five 16-B reads of the constant's record at TB (+ lidxf(g, d) records), no
 // scalar loads; the compiler schedules the reads (in order, LDS-latency).
-template <int N, bool INV, bool DFS, class LIdxF, class Fin = NoFin>
-__device__ __forceinline__ void layers_regs_lds(uint32_t (&lo)[N], uint32_t (&hi)[N], const uint32_t* TB,
+template <int N, bool INV, bool DFS, class LIdxF, class Fin = NoFin, int M = 1, bool ZERO_G0 = false>
+__device__ __forceinline__ void layers_regs_lds(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const uint32_t* TB,
                                                 LIdxF lidxf, Fin fin = Fin{}) {
     constexpr int NG = N - 1;
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
         constexpr int g = grp_at<N, INV, DFS>(I, false), d = grp_at<N, INV, DFS>(I, true);
-        const uint4* p = reinterpret_cast<const uint4*>(TB + lidxf(g, d) * kTbStride);
-        const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
-        const uint32_t t[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-        const uint32_t bv[8] = {q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w};
-        sfor<g, g + d, 1>([&](auto ii) {
-            constexpr int i = decltype(ii)::value;
-            if constexpr (INV) {
-                hi[i + d] ^= hi[i];
-                lo[i + d] ^= lo[i];
-                mul_add16_c3(lo[i], hi[i], lo[i + d], hi[i + d], t, bv);
-            } else {
-                mul_add16_c3(lo[i], hi[i], lo[i + d], hi[i + d], t, bv);
-                lo[i + d] ^= lo[i];
-                hi[i + d] ^= hi[i];
-            }
-        });
-        if constexpr (!INV && d == 1) {
+        if constexpr (!grp_mul<N, INV, ZERO_G0, DFS>(I)) {   // multiply by zero: XOR only
+            sfor<0, M, 1>([&](auto mm) {
+                sfor<g, g + d, 1>([&](auto ii) {
+                    constexpr int i = N * decltype(mm)::value + decltype(ii)::value;
+                    lo[i + d] ^= lo[i];
+                    hi[i + d] ^= hi[i];
+                });
+            });
+        } else {
+            const uint4* p = reinterpret_cast<const uint4*>(TB + lidxf(g, d) * kTbStride);
+            const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+            const uint32_t t[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+            const uint32_t bv[8] = {q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w};
+            sfor<0, M, 1>([&](auto mm) {
+                sfor<g, g + d, 1>([&](auto ii) {
+                    constexpr int i = N * decltype(mm)::value + decltype(ii)::value;
+                    if constexpr (INV) {
+                        hi[i + d] ^= hi[i];
+                        lo[i + d] ^= lo[i];
+                        mul_add16_c3(lo[i], hi[i], lo[i + d], hi[i + d], t, bv);
+                    } else {
+                        mul_add16_c3(lo[i], hi[i], lo[i + d], hi[i + d], t, bv);
+                        lo[i + d] ^= lo[i];
+                        hi[i + d] ^= hi[i];
+                    }
+                });
+            });
+        }
+        if constexpr (!INV && d == 1 && M == 1) {
             fin(std::integral_constant<int, g>{});
             fin(std::integral_constant<int, g + 1>{});
         }
@@ -585,10 +601,15 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
                 hr[16 * q + tt.value] = hi[R * tt.value + q];
             });
         });
-        layers_regs<16, true, false, R>(lr, hr, T, TB,
-                                        [&](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); });
-        layers_regs<16, false, true, R>(lr, hr, T, TB,
-                                        [&](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); });
+        auto fi = [](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); };
+        auto ff = [](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); };
+        if constexpr (CDA_RS16_LDS_B) {   // the (uniform) pass-B tables from LDS too
+            layers_regs_lds<16, true, false, decltype(fi), NoFin, R, false>(lr, hr, TB, fi);
+            layers_regs_lds<16, false, false, decltype(ff), NoFin, R, true>(lr, hr, TB, ff);
+        } else {
+            layers_regs<16, true, false, R>(lr, hr, T, TB, fi);
+            layers_regs<16, false, true, R>(lr, hr, T, TB, ff);
+        }
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
             sfor<0, 16, 1>([&](auto tt) {
