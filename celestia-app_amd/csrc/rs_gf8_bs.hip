@@ -168,30 +168,73 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
 // ---------------------------------------------------------------------------
 constexpr uint32_t kHalfLdsBytes = 8 * 8 * 4 * 64 * 4;   // E[a][b][4 planes][lane] dwords
 
-__device__ __forceinline__ uint32_t swap16(uint32_t v) {   // lane l <- lane l ^ 16
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // bit mode: and 0x1F, xor 0x10
+template <int MODE>
+__device__ __forceinline__ uint32_t swap_h(uint32_t v) {   // lane l <- its shard-parity partner
+    if constexpr (MODE == 2)
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);   // bit mode: and 0x1F, xor 0x04
+    else
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);   // bit mode: and 0x1F, xor 0x10
 }
 
-// ONE = true (small jobs, e.g. one square: config 2): one codeword per
-// workgroup, lanes 32..63 idle (their loads and stores masked off), so a
-// job of n codewords fills n workgroups instead of n / 2 -- for a single
-// k = 128 square the first launch then covers all 256 CUs instead of 128.
-template <bool ONE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job) {
-    rs_err_init(job);
+// Workgroup -> work mapping, three modes:
+//   MODE 0: two codewords per workgroup, every lane 32 columns as above.
+//   MODE 1 (small jobs, e.g. one square: config 2): one codeword per
+//     workgroup, lanes 32..63 idle (their loads and stores masked off), so a
+//     job of n codewords fills n workgroups instead of n / 2 -- for a single
+//     k = 128 square the first launch then covers all 256 CUs instead of 128.
+//   MODE 2 (batches; "slices"): Leopard is independent per byte position,
+//     so a workgroup takes EIGHT codewords restricted to one 128-byte slice
+//     [128g, 128g + 128) of every shard (lane l: codeword l/8, shard parity
+//     (l/4)&1, the 32 contiguous bytes 128g + 32(l%4)), and the workgroups of
+//     one (square, slice) unit -- every row AND every column codeword of the
+//     launch over that slice -- are numbered so that they share a block
+//     index residue mod 8, i.e. one XCD under the round-robin dispatch: the
+//     Q0 launch's row and column passes then read each 128-B line of Q0 from
+//     the fabric once (the second read hits the XCD's L2) instead of twice.
+//     Speed only; correctness does not depend on the placement.
+template <int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job,
+                                                                                                   uint32_t nsq) {
+    constexpr bool ONE = MODE == 1;
     extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = threadIdx.x & 63;
-    const uint32_t h = (l >> 4) & 1;
+    const uint32_t h = MODE == 2 ? (l >> 2) & 1 : (l >> 4) & 1;
     const uint32_t h0 = h ? 0u : 0xFFFFFFFFu;
-    const uint32_t cwg = ONE ? blockIdx.x : 2 * blockIdx.x;
-    const bool s1 = job.n_seg > 1 && cwg >= job.seg[0].n_cw;
+    // cwb: the workgroup's first codeword (uniform: segments hold whole
+    // workgroups), lane codeword cwb + lcw, lane columns col..col+15 and
+    // col+kHi..col+kHi+15
+    uint32_t sq, cwb, lcw, col;
+    if constexpr (MODE == 2) {
+        // grid: groups of 8 units x P workgroups, unit u's j-th workgroup at
+        // block 8P*(u/8) + 8j + u%8
+        const uint32_t ncw = job.seg[0].n_cw + (job.n_seg > 1 ? job.seg[1].n_cw : 0);
+        const uint32_t P = ncw / 8;
+        const uint32_t b = blockIdx.x, grp = b / (8 * P), r = b % (8 * P);
+        const uint32_t unit = grp * 8 + (r & 7), j = r >> 3;
+        sq = unit >> 2;
+        if (sq >= nsq) return;   // the last group's missing units
+        cwb = 8 * j;
+        lcw = l >> 3;
+        col = 128 * (unit & 3) + 16 * (l & 3);
+        if (job.err_init && (unit & 3) == 0 && j == 0 && threadIdx.x == 0) job.err_init[sq] = 0xFFFFFFFFu;
+    } else {
+        rs_err_init(job);
+        sq = blockIdx.y;
+        cwb = ONE ? blockIdx.x : 2 * blockIdx.x;
+        lcw = ONE ? 0u : l >> 5;
+        col = 16 * (l & 15);
+    }
+    const bool s1 = job.n_seg > 1 && cwb >= job.seg[0].n_cw;
     const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
     const bool live = !ONE || l < 32;
-    const uint32_t c = (s1 ? cwg - job.seg[0].n_cw : cwg) + (ONE ? 0u : (l >> 5));
-    const uint32_t col = 16 * (l & 15);
-    const uint8_t* src = job.src + blockIdx.y * job.src_sq;
-    uint8_t* dst = job.dst + blockIdx.y * job.dst_sq;
+    const uint32_t c = (s1 ? cwb - job.seg[0].n_cw : cwb) + lcw;
+    // the second 16 B of a lane's 32 columns: 256 bytes on (modes 0, 1: 16
+    // lanes x 16 B = 256 contiguous bytes per load), or 64 (mode 2: 4 lanes
+    // read one 64-B half of the slice's 128-B line per load)
+    constexpr uint32_t kHi = MODE == 2 ? 64 : 256;
+    const uint8_t* src = job.src + (size_t)sq * job.src_sq;
+    uint8_t* dst = job.dst + (size_t)sq * job.dst_sq;
     const uint32_t u = w;
     const uint32_t s0 = g.src_off + c * g.src_cw + col + (16 * u + h) * g.src_sh;   // shard 16u + h
     const uint32_t d0 = g.dst_off + c * g.dst_cw + col + (16 * u + h) * g.dst_sh;
@@ -205,7 +248,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         uint4 a = make_uint4(0, 0, 0, 0), b = a;
         if (live) {
             a = *reinterpret_cast<const uint4*>(src + o);
-            b = *reinterpret_cast<const uint4*>(src + o + 256);
+            b = *reinterpret_cast<const uint4*>(src + o + kHi);
         }
         R[8 * j + 0] = a.x; R[8 * j + 1] = a.y; R[8 * j + 2] = a.z; R[8 * j + 3] = a.w;
         R[8 * j + 4] = b.x; R[8 * j + 5] = b.y; R[8 * j + 6] = b.z; R[8 * j + 7] = b.w;
@@ -216,7 +259,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         for (int j = 0; j < 8; j++) {
             const uint32_t o = c0 + 2 * j * g.cpy_sh;
             *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * j], R[8 * j + 1], R[8 * j + 2], R[8 * j + 3]);
-            *reinterpret_cast<uint4*>(dst + o + 256) =
+            *reinterpret_cast<uint4*>(dst + o + kHi) =
                 make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
         }
     }
@@ -229,7 +272,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             constexpr int j = decltype(jj)::value;
             uint32_t P[8];
 #pragma unroll
-            for (int p = 0; p < 8; p++) P[p] = swap16(R[8 * j + p]);
+            for (int p = 0; p < 8; p++) P[p] = swap_h<MODE>(R[8 * j + p]);
             ifft_d1<ifft_d1_log<UU>(j)>(R + 8 * j, P, h0);
         });
         pass_a_hi<UU>(R);
@@ -273,7 +316,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             constexpr int j = decltype(jj)::value;
             uint32_t P[8];
 #pragma unroll
-            for (int p = 0; p < 8; p++) P[p] = swap16(R[8 * j + p]);
+            for (int p = 0; p < 8; p++) P[p] = swap_h<MODE>(R[8 * j + p]);
             fft_d1<fft_d1_log<UU>(j)>(R + 8 * j, P, h0);
         });
     });
@@ -283,7 +326,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         const uint32_t o = d0 + 2 * j * g.dst_sh;
         if (live) {
             *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * j], R[8 * j + 1], R[8 * j + 2], R[8 * j + 3]);
-            *reinterpret_cast<uint4*>(dst + o + 256) =
+            *reinterpret_cast<uint4*>(dst + o + kHi) =
                 make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
         }
     }
@@ -316,8 +359,9 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
         }();
         static bool attr = false;
         if (lds > 64 * 1024 && !attr) {
-            for (const void* f : {reinterpret_cast<const void*>(rs8_bs_half_kernel<false>),
-                                  reinterpret_cast<const void*>(rs8_bs_half_kernel<true>)}) {
+            for (const void* f : {reinterpret_cast<const void*>(rs8_bs_half_kernel<0>),
+                                  reinterpret_cast<const void*>(rs8_bs_half_kernel<1>),
+                                  reinterpret_cast<const void*>(rs8_bs_half_kernel<2>)}) {
                 hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
             }
@@ -331,10 +375,19 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
             return e ? atoi(e) : -1;
         }();
         const bool one = one_env >= 0 ? one_env != 0 : (uint64_t)ncw * n < 2u * 256u;
+        // batches: XCD-aware 128-B slices (CDA_RS8_SLICE=0 turns them off, A/B knob)
+        static const int slice_env = [] {
+            const char* e = getenv("CDA_RS8_SLICE");
+            return e ? atoi(e) : 1;
+        }();
+        const bool slice = !one && slice_env != 0 && j.seg[0].n_cw % 8 == 0 &&
+                           (j.n_seg < 2 || j.seg[1].n_cw % 8 == 0);
         if (one)
-            hipLaunchKernelGGL(rs8_bs_half_kernel<true>, dim3(ncw, n), dim3(512), lds, s, j);
+            hipLaunchKernelGGL(rs8_bs_half_kernel<1>, dim3(ncw, n), dim3(512), lds, s, j, n);
+        else if (slice)
+            hipLaunchKernelGGL(rs8_bs_half_kernel<2>, dim3((4 * n + 7) / 8 * ncw), dim3(512), lds, s, j, n);
         else
-            hipLaunchKernelGGL(rs8_bs_half_kernel<false>, dim3(ncw / 2, n), dim3(512), lds, s, j);
+            hipLaunchKernelGGL(rs8_bs_half_kernel<0>, dim3(ncw / 2, n), dim3(512), lds, s, j, n);
         return hipGetLastError();
     }
     const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);

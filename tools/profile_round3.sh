@@ -5,7 +5,7 @@
 #   k = 512: one square per step (config 3)
 # kernel trace + stats, then separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ
 # issue counters; SQ wait counters), summarised by tools/pmc_summary3.py into
-# gpurun_out/<tag>_pmc.json.  Usage: tools/profile_round3.sh <tag>
+# gpurun_out/<tag>_pmc.json.  Usage: [KS="128"] tools/profile_round3.sh <tag>
 set -o pipefail
 TAG=${1:-r03}
 R=$GRAFT_REPO_ROOT
@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 
 SUM=$R/gpurun_out/${TAG}_pmc.json
 rm -f $SUM
-for K in 128 512; do
+for K in ${KS:-128 512}; do
   OUT=$R/gpurun_out/prof_${TAG}_k$K
   rm -rf $OUT; mkdir -p $OUT
   if [ $K = 128 ]; then
