@@ -587,11 +587,12 @@ constexpr uint32_t kPairMaxParents = 128;   // 256 lanes: one wave per SIMD of t
 template <int R0>
 __device__ __forceinline__ void pair_rounds16(uint32_t (&v)[4], const uint32_t (&kw)[16], bool A) {
     const uint32_t r1 = A ? 2u : 6u, r2 = A ? 13u : 11u, r3 = A ? 22u : 25u;
+    const uint32_t mA = pair_mask();
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         const uint32_t S = xor3(__builtin_amdgcn_alignbit(v[0], v[0], r1), __builtin_amdgcn_alignbit(v[0], v[0], r2),
                                 __builtin_amdgcn_alignbit(v[0], v[0], r3));
-        const uint32_t F = pair_sel(ch(v[0], v[1], v[2]), maj(v[0], v[1], v[2]));
+        const uint32_t F = pair_chmaj(v[0], v[1], v[2], mA);
         const uint32_t Y = pair_sel(v[3] + kw[i], 0u);
         const uint32_t T = add3(S, F, Y);
         const uint32_t nv = pair_add(T, pair_sel(T, v[3]));

@@ -97,13 +97,14 @@ CDA_HD void sha_compress(ShaState& s, uint32_t w[16]) {
 // active, so a chain of dependent compressions costs its instruction count.
 // Lanes 2j (e-side: holds e f g h) and 2j+1 (a-side: a b c d) of a pair run
 // ONE instruction stream: per-lane rotate amounts make Sigma1 / Sigma0 (and
-// the schedule's sigma1 / sigma0) one alignbit triple; Ch / Maj one select;
+// the schedule's sigma1 / sigma0) one alignbit triple; Ch / Maj one Ch over
+// a per-lane input (pair_chmaj);
 // the pair exchanges T1 and d with a DPP quad_perm swap:
 //   e-side:  T = Sigma1 + Ch + (h + K + W) = T1,  e' = T + d(partner)
 //   a-side:  T = Sigma0 + Maj             = T2,  a' = T + T1(partner)
 // Schedule: x = w[t-2] (e-side) / w[t-15] (a-side); u = sigma + w[t-7] +
-// w[t-16]; w[t] = u + sigma(partner).  12 ops per round and 7 per schedule
-// word: 1 104 instructions per compression instead of 1 384.  Both lanes of
+// w[t-16]; w[t] = u + sigma(partner).  11 ops per round and 7 per schedule
+// word: 1 040 instructions per compression instead of 1 384.  Both lanes of
 // a pair must be active and hold the same message words.
 // ---------------------------------------------------------------------------
 struct ShaPair {
@@ -131,6 +132,15 @@ CDA_HD uint32_t pair_sel(uint32_t e_val, uint32_t a_val) {
     return r;
 }
 
+// Ch on the e-side lane, Maj on the a-side lane, in two ops instead of
+// three (two bitop3 + select): Maj(a, b, c) = Ch(a ^ c, b, c), so both lanes
+// run Ch(v0 ^ (v2 & mA), v1, v2) with mA = the a-side lane mask (0 on the
+// e-side lane, all ones on the a-side lane; pair_mask()).
+CDA_HD uint32_t pair_mask() { return pair_sel(0u, 0xFFFFFFFFu); }
+CDA_HD uint32_t pair_chmaj(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t mA) {
+    return ch(__builtin_amdgcn_bitop3_b32(v0, v2, mA, 0x78), v1, v2);   // 0x78: a ^ (b & c)
+}
+
 CDA_HD void sha_pair_init(ShaPair& s, bool A) {
     s.h[0] = A ? 0x6a09e667u : 0x510e527fu;
     s.h[1] = A ? 0xbb67ae85u : 0x9b05688cu;
@@ -142,6 +152,7 @@ CDA_HD void sha_pair_compress(ShaPair& s, uint32_t w[16], bool A) {
     constexpr uint32_t K[64] = CDA_SHA_K;
     const uint32_t r1 = A ? 2u : 6u, r2 = A ? 13u : 11u, r3 = A ? 22u : 25u;   // Sigma0 / Sigma1
     const uint32_t q1 = A ? 7u : 17u, q2 = A ? 18u : 19u, q3 = A ? 3u : 10u;   // sigma0 / sigma1
+    const uint32_t mA = pair_mask();
     uint32_t v0 = s.h[0], v1 = s.h[1], v2 = s.h[2], v3 = s.h[3];
 #pragma unroll
     for (int i = 0; i < 64; i++) {
@@ -165,7 +176,7 @@ CDA_HD void sha_pair_compress(ShaPair& s, uint32_t w[16], bool A) {
         }
         const uint32_t S = xor3(__builtin_amdgcn_alignbit(v0, v0, r1), __builtin_amdgcn_alignbit(v0, v0, r2),
                                 __builtin_amdgcn_alignbit(v0, v0, r3));
-        const uint32_t F = pair_sel(ch(v0, v1, v2), maj(v0, v1, v2));
+        const uint32_t F = pair_chmaj(v0, v1, v2, mA);
         const uint32_t Y = pair_sel(v3 + K[i] + wi, 0u);
         const uint32_t T = add3(S, F, Y);
         const uint32_t nv = pair_add(T, pair_sel(T, v3));
@@ -468,6 +479,7 @@ CDA_HD void sha_compress_kw(ShaState& s, const uint4 (&kw)[16]) {
 }
 CDA_HD void sha_pair_compress_kw(ShaPair& s, const uint4 (&kw)[16], bool A) {
     const uint32_t r1 = A ? 2u : 6u, r2 = A ? 13u : 11u, r3 = A ? 22u : 25u;
+    const uint32_t mA = pair_mask();
     uint32_t v0 = s.h[0], v1 = s.h[1], v2 = s.h[2], v3 = s.h[3];
 #pragma unroll
     for (int i = 0; i < 64; i++) {
@@ -475,7 +487,7 @@ CDA_HD void sha_pair_compress_kw(ShaPair& s, const uint4 (&kw)[16], bool A) {
         const uint32_t x = (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w;
         const uint32_t S = xor3(__builtin_amdgcn_alignbit(v0, v0, r1), __builtin_amdgcn_alignbit(v0, v0, r2),
                                 __builtin_amdgcn_alignbit(v0, v0, r3));
-        const uint32_t F = pair_sel(ch(v0, v1, v2), maj(v0, v1, v2));
+        const uint32_t F = pair_chmaj(v0, v1, v2, mA);
         const uint32_t Y = pair_sel(v3 + x, 0u);
         const uint32_t T = add3(S, F, Y);
         const uint32_t nv = pair_add(T, pair_sel(T, v3));
