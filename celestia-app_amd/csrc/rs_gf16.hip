@@ -627,6 +627,171 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Half-width codeword kernel (default for k = 256 / 512): TWO 512-thread
+// workgroups per codeword, workgroup H taking bytes [256H, 256H + 256) of
+// every shard (Leopard is independent per symbol position).  Each half is the
+// 16-wave schedule above with a "virtual wave" v = 2w + (lane >> 5) of 32
+// lanes in place of a hardware wave: v holds shards [S*v, S*v + S) in pass A /
+// A' and R residues in pass B, exactly as before, so the passes, constants and
+// exchanges are unchanged -- only which lanes hold what.  What changes is the
+// occupancy: at <= 128 VGPRs two independent workgroups share a CU, so one's
+// exchanges, barrier skew and codeword load / store phases are filled by the
+// other's butterflies (the full-width kernel fills a CU with one workgroup, and
+// all four waves of a SIMD stalled together at its barriers).
+// LDS per workgroup (k = 512: 74.5 KiB, two per CU): one 32 KiB exchange
+// sub-round, the records of ONE transform's K constants at a time (the IFFT's
+// for pass A, restaged with the FFT's during pass B for pass A') and the 30
+// constants of pass B.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHalfXchgBytes = 16 * 16 * 32 * 4;
+template <int K>
+constexpr uint32_t half_lds_bytes() {
+    return kHalfXchgBytes + (K + 32) * kTbStride * 4;
+}
+// one 80-B constant record (dwords 0..19 of the global 24-dword record) into LDS
+__device__ __forceinline__ void stage_record(uint32_t* dst, const uint32_t* __restrict__ tab, uint32_t idx) {
+    const uint4* s = reinterpret_cast<const uint4*>(tab + (size_t)idx * kGf16TabWords);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int q = 0; q < 5; q++) d[q] = s[q];
+}
+
+template <int K>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs16_half_kernel(
+    const uint32_t* __restrict__ tab, const RsJob job) {
+    static_assert(CDA_RS16_LDS_A, "the half-width kernel reads passes A / A' tables from LDS");
+    rs_err_init(job);
+    extern __shared__ uint32_t X[];
+    constexpr int S = K / 16;      // shards per virtual wave in pass A
+    constexpr int R = S / 16;      // residues per virtual wave in pass B
+    constexpr uint32_t kTA = kHalfXchgBytes / 4;                  // dword offset: this transform's K records
+    constexpr uint32_t kTPB = kTA + K * kTbStride;                // the 32 pass-B records
+    const Tab16 T{tab};
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = tid & 63, hv = lane >> 5, sl = lane & 31;
+    const uint32_t v = 2 * wave + hv;   // virtual wave (per lane)
+    // pass-B records: position p = gt + dt (1..15) IFFT constant K-1+S*p,
+    // position 16 + p FFT constant S*p-1; pass A: IFFT constant K-1+i at i
+    for (uint32_t i = tid; i < K; i += 512) stage_record(X + kTA + i * kTbStride, tab, K - 1 + i);
+    if (tid < 32 && (tid & 15))
+        stage_record(X + kTPB + tid * kTbStride, tab, tid < 16 ? K - 1 + S * tid : S * (tid - 16) - 1);
+    __syncthreads();
+
+    const bool s1 = job.n_seg > 1 && (blockIdx.x >> 1) >= job.seg[0].n_cw;
+    const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
+    const uint32_t c = s1 ? (blockIdx.x >> 1) - job.seg[0].n_cw : (blockIdx.x >> 1);
+    const uint8_t* src_base = job.src + (size_t)blockIdx.y * job.src_sq;
+    uint8_t* E = job.dst + (size_t)blockIdx.y * job.dst_sq;
+    // lane's lo dword in its shard (hi at +32), plus its virtual wave's shard
+    // offset: the uniform part of every address is base + (2S*wave + j)*stride
+    const uint32_t off = 256 * (blockIdx.x & 1) + 64 * (sl >> 3) + 4 * (sl & 7);
+    const uint32_t ss = g.src_sh, ds = g.dst_sh;
+    const uint32_t lsrc = off + S * hv * ss, ldst = off + S * hv * ds, lcpy = off + S * hv * g.cpy_sh;
+    const uint32_t s0 = g.src_off + c * g.src_cw, d0 = g.dst_off + c * g.dst_cw;
+    const uint32_t c0 = g.cpy_off == kNoCopy ? kNoCopy : g.cpy_off + c * g.cpy_cw;
+    auto ld = [&](const uint8_t* base, uint32_t o, uint32_t& l, uint32_t& h) {
+        asm volatile("" : "+s"(o));
+        const uint8_t* p = base + o;
+        l = *reinterpret_cast<const uint32_t*>(p + lsrc);
+        h = *reinterpret_cast<const uint32_t*>(p + lsrc + 32);
+    };
+    auto st = [&](uint8_t* base, uint32_t o, uint32_t lo_off, uint32_t l, uint32_t h) {
+        asm volatile("" : "+s"(o));
+        uint8_t* p = base + o;
+        *reinterpret_cast<uint32_t*>(p + lo_off) = l;
+        *reinterpret_cast<uint32_t*>(p + lo_off + 32) = h;
+    };
+
+    uint32_t lo[S], hi[S];
+    auto xbar = [] { __syncthreads(); };
+    // exchange sub-round buffer [src v][dst v][32 lanes]; lo and hi registers
+    // of a round move in two sub-rounds.  Round q moves registers R*jj + q of
+    // virtual wave t to virtual wave jj (in place: pass B's residue q lives in
+    // registers {R*t + q}).
+    auto xw = [&](uint32_t src_v, uint32_t dst_v) -> uint32_t& { return X[(src_v * 16 + dst_v) * 32 + sl]; };
+    auto xchg_a_to_b = [&]() {
+        sfor<0, R * 2, 1>([&](auto qh) {
+            constexpr int q = decltype(qh)::value / 2, hh = decltype(qh)::value % 2;
+            if (decltype(qh)::value) xbar();
+            sfor<0, 16, 1>([&](auto jj) {
+                constexpr int j = R * decltype(jj)::value + q;
+                xw(v, jj.value) = hh ? hi[j] : lo[j];
+            });
+            xbar();
+            sfor<0, 16, 1>([&](auto tt) {
+                constexpr int j = R * decltype(tt)::value + q;
+                (hh ? hi[j] : lo[j]) = xw(tt.value, v);
+            });
+        });
+    };
+    auto xchg_b_to_a = [&]() {
+        sfor<0, R * 2, 1>([&](auto qh) {
+            constexpr int q = decltype(qh)::value / 2, hh = decltype(qh)::value % 2;
+            xbar();
+            sfor<0, 16, 1>([&](auto tt) {
+                constexpr int j = R * decltype(tt)::value + q;
+                xw(tt.value, v) = hh ? hi[j] : lo[j];
+            });
+            xbar();
+            sfor<0, 16, 1>([&](auto jj) {
+                constexpr int j = R * decltype(jj)::value + q;
+                (hh ? hi[j] : lo[j]) = xw(v, jj.value);
+            });
+        });
+    };
+
+    // per-lane LDS base of the virtual wave's records (a VGPR: v is per lane)
+    const uint32_t* TBv = X + kTA + kTbStride * S * v;
+    // ---------------- pass A: IFFT d = 1 .. S/2 -------------------------
+    const uint32_t wb = 2 * S * wave;
+    sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (wb + jj.value) * ss, lo[jj.value], hi[jj.value]); });
+    if (c0 != kNoCopy) {
+        sfor<0, S, 1>([&](auto jj) { st(E, c0 + (wb + jj.value) * g.cpy_sh, lcpy, lo[jj.value], hi[jj.value]); });
+    }
+    layers_regs_lds<S, true, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d); });
+    xchg_a_to_b();
+    // every wave is past pass A (the exchange's barriers): restage the
+    // transform records with the FFT's constants 0..K-1 for pass A' (the
+    // B -> A exchange's first barrier publishes them)
+    for (uint32_t i = tid; i < K; i += 512) stage_record(X + kTA + i * kTbStride, tab, i);
+    // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
+    {
+        uint32_t lr[R * 16], hr[R * 16];
+        sfor<0, R, 1>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            sfor<0, 16, 1>([&](auto tt) {
+                lr[16 * q + tt.value] = lo[R * tt.value + q];
+                hr[16 * q + tt.value] = hi[R * tt.value + q];
+            });
+        });
+        const uint32_t* TBB = X + kTPB;
+        auto fi = [](int gt, int dt) { return (uint32_t)(K - 1 + S * gt + S * dt); };
+        auto ff = [](int gt, int dt) { return (uint32_t)(S * gt + S * dt - 1); };
+        auto lfi = [](int gt, int dt) { return (uint32_t)(gt + dt); };
+        auto lff = [](int gt, int dt) { return (uint32_t)(16 + gt + dt); };
+        if constexpr (CDA_RS16_LDS_B) {
+            layers_regs_lds<16, true, false, decltype(lfi), NoFin, R, false>(lr, hr, TBB, lfi);
+            layers_regs_lds<16, false, false, decltype(lff), NoFin, R, true>(lr, hr, TBB, lff);
+        } else {
+            layers_regs<16, true, false, R>(lr, hr, T, TBB, fi, NoFin{}, lfi);
+            layers_regs<16, false, true, R>(lr, hr, T, TBB, ff, NoFin{}, lff);
+        }
+        sfor<0, R, 1>([&](auto qq) {
+            constexpr int q = decltype(qq)::value;
+            sfor<0, 16, 1>([&](auto tt) {
+                lo[R * tt.value + q] = lr[16 * q + tt.value];
+                hi[R * tt.value + q] = hr[16 * q + tt.value];
+            });
+        });
+    }
+    xchg_b_to_a();
+    // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
+    auto store_j = [&](auto jj) { st(E, d0 + (wb + jj.value) * ds, ldst, lo[jj.value], hi[jj.value]); };
+    layers_regs_lds<S, false, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d - 1); }, store_j);
+}
+
+// ---------------------------------------------------------------------------
 // LDS-staged log/exp kernel (any k with k*64 B of LDS, any shard length)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t mul16(const uint16_t* __restrict__ lg, const uint16_t* __restrict__ ex, uint32_t y,
@@ -726,6 +891,22 @@ hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)cw_lds_bytes<K>());
         if (e != hipSuccess) return e;
         attr = true;
+    }
+    // CDA_RS16_HALF=0: the full-width one-workgroup-per-codeword kernel (A/B)
+    static const bool half = [] {
+        const char* e = getenv("CDA_RS16_HALF");
+        return e ? atoi(e) != 0 : true;
+    }();
+    if (half) {
+        static bool hattr = false;
+        if (!hattr) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs16_half_kernel<K>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)half_lds_bytes<K>());
+            if (e != hipSuccess) return e;
+            hattr = true;
+        }
+        hipLaunchKernelGGL(rs16_half_kernel<K>, dim3(2 * ncw, n), dim3(512), half_lds_bytes<K>(), s, t.chunk, j);
+        return hipGetLastError();
     }
     hipLaunchKernelGGL(rs16_cw_kernel<K>, dim3(ncw, n), dim3(1024), cw_lds_bytes<K>(), s, t.chunk, j);
     return hipGetLastError();

@@ -380,8 +380,12 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
             const char* e = getenv("CDA_RS8_SLICE");
             return e ? atoi(e) : 1;
         }();
-        const bool slice = !one && slice_env != 0 && j.seg[0].n_cw % 8 == 0 &&
-                           (j.n_seg < 2 || j.seg[1].n_cw % 8 == 0);
+        // only where two segments read the same bytes (the Q0 launch: rows
+        // and columns of Q0); the Q3 launch (rows of Q2, no re-read) runs
+        // faster in mode 0 (3.17 vs 3.43 ms per 1024 squares, while the Q0
+        // launch gains 6.06 -> 5.49; profiles/r03g/slice_ab.txt)
+        const bool slice = !one && slice_env != 0 && j.n_seg == 2 && j.seg[0].n_cw % 8 == 0 &&
+                           j.seg[1].n_cw % 8 == 0;
         if (one)
             hipLaunchKernelGGL(rs8_bs_half_kernel<1>, dim3(ncw, n), dim3(512), lds, s, j, n);
         else if (slice)

@@ -7,7 +7,8 @@ inline asm and waits for it explicitly one group later, so the compiler does
 not know the destination SGPRs are written asynchronously.  Any instruction
 that reads or writes those SGPRs (a spill, a copy) between the load and the
 next `s_waitcnt lgkmcnt(0)` would see stale data.  This compiles the file to
-gfx950 assembly and scans every rs16_cw_kernel instantiation.
+gfx950 assembly and scans every rs16_cw_kernel / rs16_half_kernel
+instantiation.
 
 Usage: python tools/check_sload_hazards.py  (exit 1 on a hazard)
 """
@@ -31,7 +32,7 @@ def sregs(text: str) -> set:
 
 def scan(asm: str) -> dict:
     res = {}
-    for m in re.finditer(r"^(_ZN3cda\w*rs16_cw_kernel\w*):(.*?)s_endpgm", asm, re.S | re.M):
+    for m in re.finditer(r"^(_ZN3cda\w*rs16_(?:cw|half)_kernel\w*):(.*?)s_endpgm", asm, re.S | re.M):
         pending, loads, hazards = set(), 0, []
         for ln in m.group(2).splitlines():
             t = ln.split(";")[0].strip()
@@ -69,7 +70,7 @@ def main() -> int:
             print("   ", t)
         bad += len(hz)
     if not res:
-        print("no rs16_cw_kernel found")
+        print("no rs16 codeword kernel found")
         return 1
     return 1 if bad else 0
 
