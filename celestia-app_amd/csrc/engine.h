@@ -235,8 +235,13 @@ class Engine {
     std::string pending_stages() const;
     // levels of the forests down to `stop` nodes per tree (f[i].in then
     // describes that level); stop = 1 runs them all
+    // (subtrees: the levels may run as one fused subtree launch, whose roots
+    // land in bufA whatever the level count -- only for callers that take
+    // f[i].in as it comes back, never the ping-pong parity)
     int run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
-                    uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop = 1);
+                    uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop = 1,
+                    bool subtrees = false);
+    int subtree_min_ = 8;   // CDA_SUBTREE: fused subtree levels when n_in / stop >= this (0 = off)
     uint32_t top_fuse_nodes(uint32_t W, uint32_t n) const;
     int top_fuse_ = -1;   // CDA_TOP_FUSE (tuning / A-B): -1 auto, 0 off, N = nodes per tree
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,
@@ -287,7 +292,7 @@ class Engine {
     int dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s);
     void dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]);
     int dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
-                  const Forest (&f)[2], Forest (&post)[2], hipStream_t s);
+                  const Forest (&f)[2], Forest (&post)[2], hipStream_t s, bool subtrees = false);
     int dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const Forest (&f)[2], uint8_t* d_roots,
                    uint32_t* d_err, int32_t* d_status, hipStream_t s);
     int enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,

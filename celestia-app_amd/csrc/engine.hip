@@ -171,6 +171,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
+    if (const char* env = getenv("CDA_SUBTREE")) subtree_min_ = atoi(env);
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
@@ -248,8 +249,12 @@ uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n) const {
 void Engine::order_begin(hipStream_t s) {
     if (!order_used_) return;
     // the previous calls' work is complete (without a fault): nothing of it can
-    // surface later
-    if (hipEventQuery(order_ev_) == hipSuccess) pending_.clear();
+    // surface later, and there is nothing to order after (no wait packet ahead
+    // of this call's first launch: the latency path's calls find it complete)
+    if (hipEventQuery(order_ev_) == hipSuccess) {
+        pending_.clear();
+        return;
+    }
     (void)hipStreamWaitEvent(s, order_ev_, 0);
 }
 
@@ -322,9 +327,43 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
 // Run every level of `f` (n_forest forests of n_in leaves each) ping-ponging
 // between two scratch buffers; the first level reads f[i].in.
 int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
-                        uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop) {
+                        uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop, bool subtrees) {
     uint8_t* out = bufA;
     int rc;
+    // The levels down to `stop` as one fused subtree launch (nmt.hip
+    // subtree_kernel): a lane per (n_in / stop)-leaf subtree.  Its roots and
+    // per-lane stacks need n_trees * stop * log2(n_in / stop) slots of each
+    // forest's output region (out_off apart; buf_sq per square).
+    if (subtrees && subtree_min_ > 0 && stop >= 2 && n_in / stop >= (uint32_t)subtree_min_ && n_in % stop == 0) {
+        const uint32_t slog = (uint32_t)__builtin_ctz(n_in / stop);
+        bool fits = true;
+        for (uint32_t i = 0; i < n_forest; i++) {
+            const uint64_t need = (uint64_t)f[i].n_trees * stop * slog * kSlot;
+            const uint64_t room = n_forest > 1 ? out_off[1] - out_off[0] : buf_sq;
+            fits = fits && need <= room && f[i].n_trees % 64 == 0;
+        }
+        // only where THIS launch holds >= a wave per SIMD on its own: with the
+        // batch split over two streams (n <= 256) each half-size launch ran
+        // at about half the wide levels' rate (k = 512 x 2: 2.07 -> 2.51 ms,
+        // k = 128 x 16: 0.93 -> 1.11 ms, profiles/r03k/batch_ab.txt), while one
+        // k = 512 square gains 1-2 % (lat_ab.txt)
+        uint64_t lanes = 0;
+        for (uint32_t i = 0; i < n_forest; i++) lanes += (uint64_t)n * f[i].n_trees * stop;
+        if (fits && lanes >= 65536) {
+            for (uint32_t i = 0; i < n_forest; i++) {
+                f[i].out = out + out_off[i];
+                f[i].out_sq = buf_sq;
+            }
+            if ((rc = check(launch_subtrees(f, n_forest, n_in, stop, n, s), "nmt subtrees"))) return rc;
+            for (uint32_t i = 0; i < n_forest; i++) {
+                f[i].in = out + out_off[i];
+                f[i].in_sq = buf_sq;
+                f[i].tree_stride = stop;
+                f[i].node_stride = 1;
+            }
+            return CDA_OK;
+        }
+    }
     for (uint32_t m = n_in; m >= 2 && m > stop; m /= 2) {
         for (uint32_t i = 0; i < n_forest; i++) {
             f[i].out = out + out_off[i];
@@ -379,7 +418,7 @@ void Engine::dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&
 // [i0, i0 + m).  f: the batch's forests from dah_forests; on return `post`
 // describes (for the whole batch) the level the chunk stopped at.
 int Engine::dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
-                      const Forest (&f)[2], Forest (&post)[2], hipStream_t s) {
+                      const Forest (&f)[2], Forest (&post)[2], hipStream_t s, bool subtrees) {
     const uint32_t W = 2 * k;
     const uint64_t slots_sq = (uint64_t)W * W * kSlot, eds_sq = (uint64_t)W * W * kShare;
     int rc;
@@ -399,7 +438,7 @@ int Engine::dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m,
         mark_begin(kStageLevels, s);
         const uint64_t off[2] = {0, slots_sq / 2};
         if ((rc = run_forests(fc, 2, W, m, lvl_.as<uint8_t>() + i0 * slots_sq, leaf_.as<uint8_t>() + i0 * slots_sq,
-                              slots_sq, off, s, stop)))
+                              slots_sq, off, s, stop, subtrees)))
             return rc;
         mark_end(s);
     }
@@ -509,7 +548,7 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
                 if ((rc = check(hipStreamWaitEvent(q, go, 0), "hipStreamWaitEvent"))) return rc;
             }
             Forest pp[2];
-            if ((rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q))) return rc;
+            if ((rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q, true))) return rc;
             if ((rc = dah_finish(k, i0, i1 - i0, stop, pp, d_roots, d_err, d_status, q))) return rc;
             if (p && (rc = check(hipEventRecord(sync_event(p), q), "hipEventRecord"))) return rc;
         }
@@ -517,7 +556,7 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
             if ((rc = check(hipStreamWaitEvent(s, sync_event(p), 0), "hipStreamWaitEvent"))) return rc;
         return CDA_OK;
     }
-    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s))) return rc;
+    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s, true))) return rc;
     return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
 }
 

@@ -308,6 +308,100 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
 }
 
 // ---------------------------------------------------------------------------
+// Fused subtree levels (latency-shaped jobs: k = 256 / 512 squares, a few per
+// call).  Where a job's levels drop from many waves per SIMD to one within a
+// few launches (k = 512, one square: 16, 8, 4, 2, 1), the per-level launches
+// pay a drain tail and a boundary each, and the last ones run below one wave
+// per SIMD.  Here ONE lane takes a whole S-leaf subtree of one tree and hashes
+// its S - 1 nodes in post order -- one node per loop iteration, the same
+// instruction stream for every lane, so the loop is uniform -- and the job
+// holds >= 1 wave per SIMD (the host picks S = n_in / top with top from
+// top_fuse_nodes, so lanes = n * 2W * top >= 65 536).  A lone wave issues an
+// instruction every ~4.25 cycles, about the rate of a SIMD saturated with the
+// same mixed stream, so these chains run at the wide
+// launches' compression rate without their tails.  The operands of the next
+// iteration (a leaf pair, or a stored left sibling) are loaded one iteration
+// ahead; pending left siblings go to a per-lane stack in the forest's output
+// buffer behind the subtree roots (written and read by the same lane).  A
+// wave is 64 consecutive trees of one subtree index, so the parity
+// mid-state branch of hash_node stays uniform.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx,
+                                                      uint32_t nsq, uint32_t nblocks) {
+    const uint32_t S = 1u << slog;
+    const uint32_t top = n_in >> slog;   // subtree roots per tree
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint32_t bx = b % nbx, r = b / nbx;
+        const size_t sq = r % nsq;
+        const Forest& F = fs.f[r / nsq];
+        const uint32_t lanes = F.n_trees * top;
+        const uint32_t idx = bx * 256 + threadIdx.x;
+        if (idx >= lanes) continue;
+        const uint32_t t = idx % F.n_trees, s = idx / F.n_trees;
+        const uint8_t* in = F.in + sq * F.in_sq + ((size_t)t * F.tree_stride + (size_t)s * S * F.node_stride) * kSlot;
+        const size_t leaf_step = (size_t)F.node_stride * kSlot;
+        uint8_t* out = F.out + sq * F.out_sq;
+        // pending left sibling at level l (1 .. slog-1): one slot per lane and
+        // level behind the `lanes` subtree-root slots
+        auto stack_slot = [&](uint32_t l) -> uint8_t* {
+            return out + ((size_t)lanes + (size_t)(l - 1) * lanes + idx) * kSlot;
+        };
+        // next operands as RAW little-endian words: byte-swapped only when
+        // they are used, one iteration later (a swap right after the load
+        // would make the compiler wait for it there)
+        uint4 nL[6], nR[6];
+        uint32_t cur[kSlotWords];
+        auto load_raw = [](const uint8_t* p, uint4 (&q)[6]) {
+            const uint4* v = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+            for (int i = 0; i < 6; i++) q[i] = v[i];
+        };
+        auto be = [](const uint4 (&q)[6], uint32_t (&w)[kSlotWords]) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                w[4 * i] = bswap32(q[i].x); w[4 * i + 1] = bswap32(q[i].y);
+                w[4 * i + 2] = bswap32(q[i].z); w[4 * i + 3] = bswap32(q[i].w);
+            }
+        };
+        load_raw(in, nL);
+        load_raw(in + leaf_step, nR);
+        uint32_t j = 0;               // next unconsumed leaf pair (pair 0 is in nL / nR)
+        uint32_t lvl = 0, pos = 0;    // level / index of cur
+#pragma unroll 1
+        for (uint32_t it = 0; it + 1 < S; it++) {
+            // cur is a right child: hash it with its stored left sibling;
+            // otherwise the next leaf pair
+            const bool merge = it > 0 && (pos & 1);
+            uint32_t L[kSlotWords], R[kSlotWords];
+            be(nL, L);
+            if (merge) {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) R[i] = bswap32(cur[i]);
+            } else {
+                be(nR, R);
+            }
+            const uint32_t nlvl = merge ? lvl + 1 : 1u, npos = merge ? pos >> 1 : j;
+            if (!merge) j++;
+            // the next iteration's memory operands, in flight during this
+            // hash: always both loads, from branch-free addresses (the stored
+            // left sibling twice before a merge; this subtree's first leaves
+            // after the last iteration), so no control-flow join forces an
+            // early wait on them
+            const bool more = it + 2 < S, sib = (npos & 1) != 0;
+            const uint8_t* pa = !more ? in : sib ? stack_slot(nlvl) : in + (size_t)(2 * j) * leaf_step;
+            const uint8_t* pb = !more ? in : sib ? pa : in + (size_t)(2 * j + 1) * leaf_step;
+            load_raw(pa, nL);
+            load_raw(pb, nR);
+            hash_node(L, R, cur);
+            if (!(npos & 1) && nlvl < slog) store_slot(stack_slot(nlvl), cur);
+            lvl = nlvl;
+            pos = npos;
+        }
+        store_slot(out + ((size_t)t * top + s) * kSlot, cur);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Fused top of the trees (latency-bound part: fewer parents than the chip has
 // wave slots).  One workgroup takes tpw trees and runs every remaining level
 // in LDS, no launch per level: the first level reads the trees' input slots
@@ -843,6 +937,23 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
     if (nblocks == 0) return hipSuccess;
     hipLaunchKernelGGL(level_kernel, dim3(hash_grid(nblocks)), dim3(256),
                        hash_lds(reinterpret_cast<const void*>(level_kernel)), s, fs, n_in, nbx, n, nblocks);
+    return hipGetLastError();
+}
+
+hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t top, uint32_t n, hipStream_t s) {
+    if (n_forest < 1 || n_forest > 2 || top < 1 || n_in % top) return hipErrorInvalidValue;
+    const uint32_t S = n_in / top;
+    if (S < 4 || (S & (S - 1))) return hipErrorInvalidValue;
+    Forest2 fs{};
+    uint32_t maxw = 0;
+    for (uint32_t i = 0; i < n_forest; i++) {
+        fs.f[i] = f[i];
+        maxw = std::max(maxw, f[i].n_trees * top);
+    }
+    const uint32_t nbx = (maxw + 255) / 256, nblocks = nbx * n * n_forest;
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(subtree_kernel, dim3(nblocks), dim3(256), 0, s, fs, n_in, (uint32_t)__builtin_ctz(S), nbx, n,
+                       nblocks);
     return hipGetLastError();
 }
 
