@@ -234,7 +234,13 @@ constexpr uint32_t kTbSrc1 = CDA_RS16_LDS_A ? 12 : 0;     // offset of the src1 
 struct TabB {   // src1 halves of one constant, [a][lo/hi] as 8 dwords
     uint4 b0, b1;
 };
-__device__ __forceinline__ TabB load_tab_b(const uint32_t* TB, uint32_t idx) {
+// plane != 0: plane-major records (chunk q of record idx at TB + 4 idx +
+// q plane dwords; rs16_half_kernel), else record-major (kTbStride apart)
+__device__ __forceinline__ TabB load_tab_b(const uint32_t* TB, uint32_t idx, uint32_t plane = 0) {
+    if (plane) {
+        const uint32_t* p = TB + 4 * idx;
+        return TabB{*reinterpret_cast<const uint4*>(p + 3 * plane), *reinterpret_cast<const uint4*>(p + 4 * plane)};
+    }
     const uint4* p = reinterpret_cast<const uint4*>(TB + idx * kTbStride + kTbSrc1);
     return TabB{p[0], p[1]};
 }
@@ -270,7 +276,8 @@ struct NoFin {   // layers_regs hook: register i holds its final value
 template <int N, bool INV, bool ZERO_G0 = false, int M = 1, bool DFS = false, class IdxF, class Fin = NoFin,
           class LIdxF = std::nullptr_t>
 __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const Tab16& T,
-                                            const uint32_t* TB, IdxF idxf, Fin fin = Fin{}, LIdxF lidxf = nullptr) {
+                                            const uint32_t* TB, IdxF idxf, Fin fin = Fin{}, LIdxF lidxf = nullptr,
+                                            uint32_t plane = 0) {
     static_assert(!(INV && ZERO_G0), "only FFT groups have structural zero skews");
     constexpr int NG = N - 1;
     // The scalar loads are issued from inline asm: the compiler treats loads
@@ -297,7 +304,7 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
     if constexpr (F0 < NG) tc = load_tabs(tab_ptr(F0c{}));
 #ifndef CDA_RS16_CHUNK2
     TabB bc{};
-    if constexpr (F0 < NG) bc = load_tab_b(TB, tab_idx(F0c{}));
+    if constexpr (F0 < NG) bc = load_tab_b(TB, tab_idx(F0c{}), plane);
 #endif
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
@@ -322,7 +329,7 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
             if constexpr (J < NG) tn = load_tabs(tab_ptr(Jc{}));
 #ifndef CDA_RS16_CHUNK2
             TabB bn;
-            if constexpr (J < NG) bn = load_tab_b(TB, tab_idx(Jc{}));
+            if constexpr (J < NG) bn = load_tab_b(TB, tab_idx(Jc{}), plane);
 #endif
             // the group's operands pass through volatile asm after the load, so
             // the scheduler cannot hoist the butterflies above it
@@ -380,7 +387,7 @@ __device__ __forceinline__ void layers_regs(uint32_t (&lo)[M * N], uint32_t (&hi
 // scalar loads; the compiler schedules the reads (in order, LDS-latency).
 template <int N, bool INV, bool DFS, class LIdxF, class Fin = NoFin, int M = 1, bool ZERO_G0 = false>
 __device__ __forceinline__ void layers_regs_lds(uint32_t (&lo)[M * N], uint32_t (&hi)[M * N], const uint32_t* TB,
-                                                LIdxF lidxf, Fin fin = Fin{}) {
+                                                LIdxF lidxf, Fin fin = Fin{}, uint32_t plane = 0) {
     constexpr int NG = N - 1;
     sfor<0, NG, 1>([&](auto II) {
         constexpr int I = decltype(II)::value;
@@ -394,8 +401,18 @@ __device__ __forceinline__ void layers_regs_lds(uint32_t (&lo)[M * N], uint32_t 
                 });
             });
         } else {
-            const uint4* p = reinterpret_cast<const uint4*>(TB + lidxf(g, d) * kTbStride);
-            const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+            uint4 q0, q1, q2, q3, q4;
+            if (plane) {   // one VGPR base, the planes as immediate offsets
+                const uint32_t* p = TB + 4 * lidxf(g, d);
+                q0 = *reinterpret_cast<const uint4*>(p);
+                q1 = *reinterpret_cast<const uint4*>(p + plane);
+                q2 = *reinterpret_cast<const uint4*>(p + 2 * plane);
+                q3 = *reinterpret_cast<const uint4*>(p + 3 * plane);
+                q4 = *reinterpret_cast<const uint4*>(p + 4 * plane);
+            } else {
+                const uint4* p = reinterpret_cast<const uint4*>(TB + lidxf(g, d) * kTbStride);
+                q0 = p[0]; q1 = p[1]; q2 = p[2]; q3 = p[3]; q4 = p[4];
+            }
             const uint32_t t[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
             const uint32_t bv[8] = {q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w};
             sfor<0, M, 1>([&](auto mm) {
@@ -644,9 +661,37 @@ __global__ __launch_bounds__(1024) void rs16_cw_kernel(const uint32_t* __restric
 // constants of pass B.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kHalfXchgBytes = 16 * 16 * 32 * 4;
+// pass A' records restaged by LDS-DMA (global_load_lds_dwordx4) instead of
+// through registers (A/B: -DCDA_RS16_GLDS=0)
+#ifndef CDA_RS16_GLDS
+#define CDA_RS16_GLDS 1
+#endif
+constexpr uint32_t kHalfPbRecords = CDA_RS16_GLDS ? 64 : 32;   // pass-B record slots (30 used)
 template <int K>
 constexpr uint32_t half_lds_bytes() {
-    return kHalfXchgBytes + (K + 32) * kTbStride * 4;
+    return kHalfXchgBytes + (K + kHalfPbRecords) * kTbStride * 4;
+}
+// 16 B from global to LDS by LDS-DMA: lane l's bytes land at lds + 16 l
+// (lds wave-uniform).  Inline asm, not the builtin: the compiler drains every
+// outstanding vector-memory op (vmcnt(0)) before the next LDS read after a
+// builtin LDS-DMA -- here the next table or exchange read, long before these
+// bytes are needed.  The caller waits for them itself (an explicit vmcnt
+// before the barrier that publishes them); the compiler's own vmcnt counts
+// stay safe, since these ops are older or extra, never fewer.  M0 is
+// compiler-reserved, so it is saved and restored in the same statement.
+// Source: a uniform base (SGPRs) + a per-lane 32-bit byte offset (one VGPR).
+__device__ __forceinline__ void glds16(const uint32_t* base, uint32_t lane_off, const uint32_t* lds) {
+    const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)lds;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(lane_off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(dst))
+        : "memory");
 }
 // one 80-B constant record (dwords 0..19 of the global 24-dword record) into LDS
 __device__ __forceinline__ void stage_record(uint32_t* dst, const uint32_t* __restrict__ tab, uint32_t idx) {
@@ -665,19 +710,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     constexpr int S = K / 16;      // shards per virtual wave in pass A
     constexpr int R = S / 16;      // residues per virtual wave in pass B
     constexpr uint32_t kTA = kHalfXchgBytes / 4;                  // dword offset: this transform's K records
-    constexpr uint32_t kTPB = kTA + K * kTbStride;                // the 32 pass-B records
+    constexpr uint32_t kTPB = kTA + K * kTbStride;                // the pass-B records
     const Tab16 T{tab};
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = tid & 63, hv = lane >> 5, sl = lane & 31;
     const uint32_t v = 2 * wave + hv;   // virtual wave (per lane)
-    // pass-B records: position p = gt + dt (1..15) IFFT constant K-1+S*p,
-    // position 16 + p FFT constant S*p-1; pass A: IFFT constant K-1+i at i
-    for (uint32_t i = tid; i < K; i += 512) stage_record(X + kTA + i * kTbStride, tab, K - 1 + i);
-    if (tid < 32 && (tid & 15))
-        stage_record(X + kTPB + tid * kTbStride, tab, tid < 16 ? K - 1 + S * tid : S * (tid - 16) - 1);
-    __syncthreads();
-
     const bool s1 = job.n_seg > 1 && (blockIdx.x >> 1) >= job.seg[0].n_cw;
     const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
     const uint32_t c = s1 ? (blockIdx.x >> 1) - job.seg[0].n_cw : (blockIdx.x >> 1);
@@ -710,7 +748,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     // virtual wave t to virtual wave jj (in place: pass B's residue q lives in
     // registers {R*t + q}).
     auto xw = [&](uint32_t src_v, uint32_t dst_v) -> uint32_t& { return X[(src_v * 16 + dst_v) * 32 + sl]; };
-    auto xchg_a_to_b = [&]() {
+    // after_first: runs once every wave is past pass A (the first barrier)
+    auto xchg_a_to_b = [&](auto after_first) {
         sfor<0, R * 2, 1>([&](auto qh) {
             constexpr int q = decltype(qh)::value / 2, hh = decltype(qh)::value % 2;
             if (decltype(qh)::value) xbar();
@@ -719,6 +758,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                 xw(v, jj.value) = hh ? hi[j] : lo[j];
             });
             xbar();
+            if constexpr (decltype(qh)::value == 0) after_first();
             sfor<0, 16, 1>([&](auto tt) {
                 constexpr int j = R * decltype(tt)::value + q;
                 (hh ? hi[j] : lo[j]) = xw(tt.value, v);
@@ -726,6 +766,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         });
     };
     auto xchg_b_to_a = [&]() {
+#if CDA_RS16_GLDS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's restage DMA (glds16)
+#endif
         sfor<0, R * 2, 1>([&](auto qh) {
             constexpr int q = decltype(qh)::value / 2, hh = decltype(qh)::value % 2;
             xbar();
@@ -742,19 +785,69 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     };
 
     // per-lane LDS base of the virtual wave's records (a VGPR: v is per lane)
-    const uint32_t* TBv = X + kTA + kTbStride * S * v;
+    const uint32_t* TBv = X + kTA + (CDA_RS16_GLDS ? 4u : kTbStride) * S * v;
+    // Records in LDS: a transform's K records at kTA (position i = the IFFT's
+    // constant K-1+i for pass A, the FFT's constant i for pass A'); pass B's
+    // at kTPB (position p = gt + dt in 1..15: IFFT constant K-1+S*p; 16 + p:
+    // FFT constant S*p-1).  An 80-B record is five 16-B chunks; with
+    // CDA_RS16_GLDS they are stored plane-major (chunk q of record i at
+    // 16 i + q * plane bytes), so one LDS-DMA wave-instruction moves chunk q
+    // of 64 consecutive records (lane = record: a per-lane source offset of
+    // 96 * lane), and a record read is still one VGPR base + immediates.
+#if CDA_RS16_GLDS
+    constexpr uint32_t kPlaneA = 4 * K, kPlaneB = 4 * kHalfPbRecords;   // dwords
+    auto dma_records = [&](uint32_t first) {
+        constexpr uint32_t kPerPlane = K / 64, kInsts = 5 * kPerPlane;
+        const uint32_t lane96 = 96 * lane;
+        for (uint32_t m = wave; m < kInsts; m += 8) {
+            const uint32_t q = m / kPerPlane, i0 = (m % kPerPlane) * 64;
+            glds16(tab + (size_t)(first + i0) * kGf16TabWords + 4 * q, lane96, X + kTA + q * kPlaneA + 4 * i0);
+        }
+    };
+#else
+    constexpr uint32_t kPlaneA = 0, kPlaneB = 0;
+#endif
     // ---------------- pass A: IFFT d = 1 .. S/2 -------------------------
     const uint32_t wb = 2 * S * wave;
+#if CDA_RS16_GLDS
+    // The tables' DMA goes out first, then the codeword's loads; the wave
+    // waits only for its DMA (vector-memory counts retire in order: all but
+    // the last min(2S, 63) loads), and pass A consumes the codeword's loads
+    // as they arrive (depth-first) instead of after all of them.
+    dma_records(K - 1);
+    if (wave < 5) {   // pass B's 64 slots (30 used; the rest get record 0): plane q = wave
+        const uint32_t pos = lane, p = pos & 15;
+        const uint32_t idx = pos >= 32 || p == 0 ? 0u : pos < 16 ? K - 1 + S * p : S * p - 1;
+        glds16(tab + 4 * wave, idx * (kGf16TabWords * 4), X + kTPB + wave * kPlaneB);
+    }
     sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (wb + jj.value) * ss, lo[jj.value], hi[jj.value]); });
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * S < 63 ? 2 * S : 63) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#else
+    sfor<0, S, 1>([&](auto jj) { ld(src_base, s0 + (wb + jj.value) * ss, lo[jj.value], hi[jj.value]); });
+    for (uint32_t i = tid; i < K; i += 512) stage_record(X + kTA + i * kTbStride, tab, K - 1 + i);
+    if (tid < 32 && (tid & 15))
+        stage_record(X + kTPB + tid * kTbStride, tab, tid < 16 ? K - 1 + S * tid : S * (tid - 16) - 1);
+    __syncthreads();
+#endif
     if (c0 != kNoCopy) {
         sfor<0, S, 1>([&](auto jj) { st(E, c0 + (wb + jj.value) * g.cpy_sh, lcpy, lo[jj.value], hi[jj.value]); });
     }
-    layers_regs_lds<S, true, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d); });
-    xchg_a_to_b();
-    // every wave is past pass A (the exchange's barriers): restage the
-    // transform records with the FFT's constants 0..K-1 for pass A' (the
-    // B -> A exchange's first barrier publishes them)
+    layers_regs_lds<S, true, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d); }, NoFin{},
+                                       kPlaneA);
+    // once every wave is past pass A (the exchange's first barrier), the
+    // transform records are restaged with the FFT's constants 0..K-1 for pass
+    // A'; the B -> A exchange's first barrier publishes them
+#if CDA_RS16_GLDS
+    // (issued after the exchange: inside it, next to 64 live data registers,
+    // the DMA's address arithmetic spilled 34 VGPRs)
+    xchg_a_to_b([] {});
+    dma_records(0);
+#else
+    xchg_a_to_b([] {});
     for (uint32_t i = tid; i < K; i += 512) stage_record(X + kTA + i * kTbStride, tab, i);
+#endif
     // ---------------- pass B: IFFT d = S .. K/2, FFT d = K/2 .. S --------
     {
         uint32_t lr[R * 16], hr[R * 16];
@@ -771,11 +864,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         auto lfi = [](int gt, int dt) { return (uint32_t)(gt + dt); };
         auto lff = [](int gt, int dt) { return (uint32_t)(16 + gt + dt); };
         if constexpr (CDA_RS16_LDS_B) {
-            layers_regs_lds<16, true, false, decltype(lfi), NoFin, R, false>(lr, hr, TBB, lfi);
-            layers_regs_lds<16, false, false, decltype(lff), NoFin, R, true>(lr, hr, TBB, lff);
+            layers_regs_lds<16, true, false, decltype(lfi), NoFin, R, false>(lr, hr, TBB, lfi, NoFin{}, kPlaneB);
+            layers_regs_lds<16, false, false, decltype(lff), NoFin, R, true>(lr, hr, TBB, lff, NoFin{}, kPlaneB);
         } else {
-            layers_regs<16, true, false, R>(lr, hr, T, TBB, fi, NoFin{}, lfi);
-            layers_regs<16, false, true, R>(lr, hr, T, TBB, ff, NoFin{}, lff);
+            layers_regs<16, true, false, R>(lr, hr, T, TBB, fi, NoFin{}, lfi, kPlaneB);
+            layers_regs<16, false, true, R>(lr, hr, T, TBB, ff, NoFin{}, lff, kPlaneB);
         }
         sfor<0, R, 1>([&](auto qq) {
             constexpr int q = decltype(qq)::value;
@@ -788,7 +881,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     xchg_b_to_a();
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
     auto store_j = [&](auto jj) { st(E, d0 + (wb + jj.value) * ds, ldst, lo[jj.value], hi[jj.value]); };
-    layers_regs_lds<S, false, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d - 1); }, store_j);
+    layers_regs_lds<S, false, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d - 1); }, store_j,
+                                        kPlaneA);
 }
 
 // ---------------------------------------------------------------------------
