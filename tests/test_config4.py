@@ -131,6 +131,46 @@ def test_config4_all_1024_squares_one_submission(ctx):
     assert list(bench.shard(0, 1, 1024)) == list(range(1024))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,rank", [(2, 1), (4, 2)])
+def test_config4_multi_gpu_shard_one_submission(ctx, world, rank):
+    """The per-GPU shard of config 4 at N = 2 and N = 4 (BASELINE.json
+    configs[3]: 1024 squares split over N GPUs): rank g's 1024 / N squares in
+    ONE in-place submission, exactly what bench.py's rank g submits (16 and 8
+    GiB arenas: offsets past 2^32 at N = 2), every data root and root digest
+    against the oracle fixtures."""
+    import torch
+
+    import bench
+    from celestia_da import testfactory
+    g = _fixture()
+    g["squares"].update(_fixture_rest()["squares"])
+    k = 128
+    n = 1024 // world
+    W = 2 * k
+    idx = list(bench.shard(rank, world, n))
+    dev = torch.device("cuda", 0)
+    eds = torch.empty((n, W, W, 512), dtype=torch.uint8, device=dev)
+    for j0, part in testfactory.random_squares(k, idx):
+        eds[j0:j0 + part.shape[0], :k, :k] = torch.from_numpy(part).to(dev).view(-1, k, k, 512)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    r, c, dr = rows.cpu().numpy(), cols.cpu().numpy(), roots.cpu().numpy()
+    bad = [(p, i) for p, i in enumerate(idx)
+           if dr[p].tobytes().hex() != g["squares"][str(i)]["data_root"]
+           or _sha(r[p].reshape(W, 90)) != g["squares"][str(i)]["row_roots_sha256"]
+           or _sha(c[p].reshape(W, 90)) != g["squares"][str(i)]["col_roots_sha256"]]
+    assert not bad, f"{len(bad)} squares differ from the oracle, first {bad[:4]}"
+    del eds
+    torch.cuda.empty_cache()
+
+
 def test_shard_partitions_config4():
     import bench
     for world in (1, 2, 4, 8):
