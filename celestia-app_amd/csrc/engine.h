@@ -235,13 +235,14 @@ class Engine {
     std::string pending_stages() const;
     // levels of the forests down to `stop` nodes per tree (f[i].in then
     // describes that level); stop = 1 runs them all
-    // (subtrees: the levels may run as one fused subtree launch, whose roots
-    // land in bufA whatever the level count -- only for callers that take
-    // f[i].in as it comes back, never the ping-pong parity)
+    // (subtrees: the first levels may run as one fused subtree launch, after
+    // which the ping-pong parity no longer follows the level count -- only for
+    // callers that take f[i].in as it comes back)
     int run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint8_t* bufA, uint8_t* bufB,
                     uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop = 1,
                     bool subtrees = false);
-    int subtree_min_ = 8;   // CDA_SUBTREE: fused subtree levels when n_in / stop >= this (0 = off)
+    int subtree_min_ = 8;   // CDA_SUBTREE: fused subtree levels of >= this many leaves (0 = off)
+    uint64_t subtree_lanes_ = 131072;   // CDA_SUBTREE_LANES: lanes a subtree launch must hold
     uint32_t top_fuse_nodes(uint32_t W, uint32_t n) const;
     int top_fuse_ = -1;   // CDA_TOP_FUSE (tuning / A-B): -1 auto, 0 off, N = nodes per tree
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,

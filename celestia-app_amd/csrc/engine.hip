@@ -172,6 +172,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
     if (const char* env = getenv("CDA_SUBTREE")) subtree_min_ = atoi(env);
+    if (const char* env = getenv("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
@@ -330,41 +331,45 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
                         uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop, bool subtrees) {
     uint8_t* out = bufA;
     int rc;
-    // The levels down to `stop` as one fused subtree launch (nmt.hip
-    // subtree_kernel): a lane per (n_in / stop)-leaf subtree.  Its roots and
-    // per-lane stacks need n_trees * stop * log2(n_in / stop) slots of each
-    // forest's output region (out_off apart; buf_sq per square).
-    if (subtrees && subtree_min_ > 0 && stop >= 2 && n_in / stop >= (uint32_t)subtree_min_ && n_in % stop == 0) {
-        const uint32_t slog = (uint32_t)__builtin_ctz(n_in / stop);
-        bool fits = true;
-        for (uint32_t i = 0; i < n_forest; i++) {
-            const uint64_t need = (uint64_t)f[i].n_trees * stop * slog * kSlot;
+    // The first levels as one fused subtree launch (nmt.hip subtree_kernel):
+    // a lane per (n_in / sub)-leaf subtree, sub the smallest node count >= stop
+    // at which the launch holds subtree_lanes_ lanes (default two waves per
+    // SIMD: a lone wave per SIMD issues at ~5.4 cycles per instruction on this
+    // chain, two interleave to the saturated rate); the levels from sub down to
+    // stop then run as per-level launches.  Roots and per-lane stacks need
+    // n_trees * sub * log2(n_in / sub) slots of each forest's output region.
+    // With the batch split over two streams (n <= 256) each launch holds only
+    // its part's lanes, so the lane bound is per launch.
+    uint32_t m0 = n_in;
+    if (subtrees && subtree_min_ > 0 && stop >= 2 && n_in % stop == 0) {
+        uint64_t per_node = 0;   // lanes per subtree root per tree
+        for (uint32_t i = 0; i < n_forest; i++) per_node += (uint64_t)n * f[i].n_trees;
+        uint32_t sub = stop;
+        while (sub < n_in && per_node * sub < subtree_lanes_) sub *= 2;
+        bool fits = per_node * sub >= subtree_lanes_ && sub < n_in && n_in / sub >= (uint32_t)subtree_min_;
+        const uint32_t slog = fits ? (uint32_t)__builtin_ctz(n_in / sub) : 0;
+        for (uint32_t i = 0; i < n_forest && fits; i++) {
+            const uint64_t need = (uint64_t)f[i].n_trees * sub * slog * kSlot;
             const uint64_t room = n_forest > 1 ? out_off[1] - out_off[0] : buf_sq;
-            fits = fits && need <= room && f[i].n_trees % 64 == 0;
+            fits = need <= room && f[i].n_trees % 64 == 0;
         }
-        // only where THIS launch holds >= a wave per SIMD on its own: with the
-        // batch split over two streams (n <= 256) each half-size launch ran
-        // at about half the wide levels' rate (k = 512 x 2: 2.07 -> 2.51 ms,
-        // k = 128 x 16: 0.93 -> 1.11 ms, profiles/r03k/batch_ab.txt), while one
-        // k = 512 square gains 1-2 % (lat_ab.txt)
-        uint64_t lanes = 0;
-        for (uint32_t i = 0; i < n_forest; i++) lanes += (uint64_t)n * f[i].n_trees * stop;
-        if (fits && lanes >= 65536) {
+        if (fits) {
             for (uint32_t i = 0; i < n_forest; i++) {
                 f[i].out = out + out_off[i];
                 f[i].out_sq = buf_sq;
             }
-            if ((rc = check(launch_subtrees(f, n_forest, n_in, stop, n, s), "nmt subtrees"))) return rc;
+            if ((rc = check(launch_subtrees(f, n_forest, n_in, sub, n, s), "nmt subtrees"))) return rc;
             for (uint32_t i = 0; i < n_forest; i++) {
                 f[i].in = out + out_off[i];
                 f[i].in_sq = buf_sq;
-                f[i].tree_stride = stop;
+                f[i].tree_stride = sub;
                 f[i].node_stride = 1;
             }
-            return CDA_OK;
+            out = bufB;
+            m0 = sub;
         }
     }
-    for (uint32_t m = n_in; m >= 2 && m > stop; m /= 2) {
+    for (uint32_t m = m0; m >= 2 && m > stop; m /= 2) {
         for (uint32_t i = 0; i < n_forest; i++) {
             f[i].out = out + out_off[i];
             f[i].out_sq = buf_sq;
