@@ -40,18 +40,9 @@ using namespace bs8;
 
 constexpr uint32_t kLdsBytes = 8 * 8 * 8 * 64 * 4;   // E[u][tt][p][lane] dwords
 
-// Timing-diagnostic builds only (tools/rs8_phase_probe.sh, wrong output):
-// CDA_RS8_PROBE=1 drops the XOR networks and transposes (memory + exchange
-// phases alone), =2 drops the global loads and stores (compute + exchange),
-// =3 drops the LDS exchanges, =4 makes the kernel a no-op (hash stages alone).
-#ifndef CDA_RS8_PROBE
-#define CDA_RS8_PROBE 0
-#endif
-constexpr bool kCompute = CDA_RS8_PROBE != 1, kMemory = CDA_RS8_PROBE != 2, kExchange = CDA_RS8_PROBE != 3;
 
 __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob job) {
     rs_err_init(job);
-    if constexpr (CDA_RS8_PROBE == 4) return;
     extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = threadIdx.x & 63;
@@ -77,18 +68,13 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
     // ---- pass A --------------------------------------------------------
 #pragma unroll
     for (int t = 0; t < 16; t++) {
-        if constexpr (!kMemory) {
-#pragma unroll
-            for (int p = 0; p < 8; p++) R[8 * t + p] = (threadIdx.x + 977u * blockIdx.x) * (8u * t + p + 1u);
-            continue;
-        }
         const uint32_t o = s0 + (16 * u + t) * g.src_sh;
         const uint4 a = *reinterpret_cast<const uint4*>(src + o);
         const uint4 b = *reinterpret_cast<const uint4*>(src + o + 256);
         R[8 * t + 0] = a.x; R[8 * t + 1] = a.y; R[8 * t + 2] = a.z; R[8 * t + 3] = a.w;
         R[8 * t + 4] = b.x; R[8 * t + 5] = b.y; R[8 * t + 6] = b.z; R[8 * t + 7] = b.w;
     }
-    if (kMemory && g.cpy_off != kNoCopy) {
+    if (g.cpy_off != kNoCopy) {
         const uint32_t c0 = g.cpy_off + c * g.cpy_cw + col;
 #pragma unroll
         for (int t = 0; t < 16; t++) {
@@ -98,15 +84,13 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
                 make_uint4(R[8 * t + 4], R[8 * t + 5], R[8 * t + 6], R[8 * t + 7]);
         }
     }
-    if constexpr (kCompute) {
 #pragma unroll
-        for (int t = 0; t < 16; t++) transpose8(R + 8 * t);
-        with_u_chain(ud, [&](auto U) { pass_a<decltype(U)::value>(R); });
-    }
+    for (int t = 0; t < 16; t++) transpose8(R + 8 * t);
+    with_u_chain(ud, [&](auto U) { pass_a<decltype(U)::value>(R); });
 
     // ---- A -> B: round r moves t = 8r + tt (tt = 0..7) ---------------------
 #pragma unroll
-    for (int r = 0; r < (kExchange ? 2 : 0); r++) {
+    for (int r = 0; r < 2; r++) {
         if (r) __syncthreads();
 #pragma unroll
         for (int tt = 0; tt < 8; tt++)
@@ -119,13 +103,11 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
             for (int p = 0; p < 8; p++) R[64 * r + 8 * uu + p] = E[((uu * 8 + w) * 8 + p) * 64 + l];
     }
     // ---- pass B: units t = w (R[0..64)) and t = w + 8 (R[64..128)) ---------
-    if constexpr (kCompute) {
-        pass_b(R);
-        pass_b(R + 64);
-    }
+    pass_b(R);
+    pass_b(R + 64);
     // ---- B -> C ------------------------------------------------------------
 #pragma unroll
-    for (int r = 0; r < (kExchange ? 2 : 0); r++) {
+    for (int r = 0; r < 2; r++) {
         __syncthreads();
 #pragma unroll
         for (int uu = 0; uu < 8; uu++)
@@ -138,17 +120,10 @@ __global__ __launch_bounds__(512) CDA_RS8_ATTR void rs8_bs_kernel(const RsJob jo
             for (int p = 0; p < 8; p++) R[8 * (8 * r + tt) + p] = E[((u * 8 + tt) * 8 + p) * 64 + l];
     }
     // ---- pass C --------------------------------------------------------
-    if constexpr (kCompute) with_u_chain(ud, [&](auto U) { pass_c<decltype(U)::value>(R); });
-    if constexpr (!kMemory) {   // keep every result live: a store no input can trigger
-        uint32_t acc = 0;
-#pragma unroll
-        for (int i = 0; i < 128; i++) acc ^= R[i] * (uint32_t)(2 * i + 1);
-        if (acc == 0x9E3779B9u && threadIdx.x == 511u) dst[d0] = (uint8_t)acc;
-        return;
-    }
+    with_u_chain(ud, [&](auto U) { pass_c<decltype(U)::value>(R); });
 #pragma unroll
     for (int t = 0; t < 16; t++) {
-        if constexpr (kCompute) transpose8(R + 8 * t);
+        transpose8(R + 8 * t);
         const uint32_t o = d0 + (16 * u + t) * g.dst_sh;
         *reinterpret_cast<uint4*>(dst + o) = make_uint4(R[8 * t], R[8 * t + 1], R[8 * t + 2], R[8 * t + 3]);
         *reinterpret_cast<uint4*>(dst + o + 256) = make_uint4(R[8 * t + 4], R[8 * t + 5], R[8 * t + 6], R[8 * t + 7]);
