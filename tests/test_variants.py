@@ -5,7 +5,8 @@ process, so the non-default forms are only reachable from a fresh process:
   * CDA_RS16_HALF=0 -- the full-width GF(2^16) codeword kernel (one 1024-thread
     workgroup per codeword) instead of the default two half-width workgroups;
   * CDA_RS8_SLICE=0 -- the k = 128 Q0 launch of a batch without the XCD-aware
-    128-byte slices (mode 0, two codewords per workgroup).
+    128-byte slices (mode 0, two codewords per workgroup);
+  * CDA_RS8_BS=1 -- round 1's four-codeword k = 128 encoder.
 Each child extends squares of the committed fixtures and compares data roots
 and EDS / root digests (tests/golden/k512.json, config4_k128.json; generated
 by oracle/gen_config4.py from the C oracle).  Reference: the Leopard encoders
@@ -68,12 +69,14 @@ def test_full_width_gf16_kernel_matches_fixture():
         assert got[i]["data_root"] == g[str(i)]["data_root"], i
 
 
-@pytest.mark.parametrize("slice_mode", ["0", "1"])
-def test_gf8_q0_modes_match_fixture(slice_mode):
+@pytest.mark.parametrize("env", [{"CDA_RS8_SLICE": "0"}, {"CDA_RS8_SLICE": "1"}, {"CDA_RS8_BS": "1"}],
+                         ids=["mode0", "slices", "round1_kernel"])
+def test_gf8_q0_modes_match_fixture(env):
     """16 squares in one submission (the batch path: slice mode 2 unless
-    CDA_RS8_SLICE=0) against config 4's fixture (squares 0..15)."""
+    CDA_RS8_SLICE=0; CDA_RS8_BS=1 is round 1's four-codeword kernel) against
+    config 4's fixture (squares 0..15)."""
     g = json.load(open(os.path.join(HERE, "golden", "config4_k128.json")))["squares"]
-    got = _run({"CDA_RS8_SLICE": slice_mode}, 128, 16)
+    got = _run(env, 128, 16)
     for i in range(16):
         want = g[str(i)]
         assert got[i]["status"] == 0
