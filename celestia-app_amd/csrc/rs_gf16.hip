@@ -702,14 +702,15 @@ __device__ __forceinline__ void stage_record(uint32_t* dst, const uint32_t* __re
 }
 
 // Timing probe (tools/rs16_phases.py; never in the product build; outputs
-// unchanged): thread 0 of four sampled workgroups stamps s_memtime at the
-// kernel's phase boundaries.
+// unchanged): thread 0 of four sampled workgroups (the grid's first two and
+// last two) stamps s_memtime at the kernel's phase boundaries.
 #ifdef CDA_RS16_PHASES
 __device__ unsigned long long g_rs16_phase[4][8];
 #define RS16_MARK(i)                                                                                      \
     do {                                                                                                  \
         const uint32_t b_ = blockIdx.x;                                                                   \
-        const int slot_ = b_ == 0 ? 0 : b_ == 1 ? 1 : b_ == 1200 ? 2 : b_ == 1201 ? 3 : -1;               \
+        const uint32_t e_ = gridDim.x;                                                                    \
+        const int slot_ = b_ == 0 ? 0 : b_ == 1 ? 1 : b_ == e_ - 2 ? 2 : b_ == e_ - 1 ? 3 : -1;           \
         if (slot_ >= 0 && blockIdx.y == 0 && threadIdx.x == 0)                                            \
             g_rs16_phase[slot_][i] = __builtin_amdgcn_s_memtime();                                        \
     } while (0)

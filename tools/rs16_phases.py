@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """Phase timeline of rs16_half_kernel<512> from a -DCDA_RS16_PHASES build
 (tools/build_variant.sh rs16ph -DCDA_RS16_PHASES; run with CDA_LIB=<that>):
-thread 0 of workgroups 0, 1 (the two halves of codeword 0, launch start) and
-1200, 1201 (mid-launch) stamps s_memtime (shader cycles) at: start, tables
-staged + codeword loaded, pass A done, A->B exchange done, pass B done,
-B->A exchange done, pass A' (and its stores) issued.  One k = 512 square; the
-sampled launch is the LAST RS launch of the call (Q2 -> Q3, 1024 workgroups:
-1200/1201 do not exist there, so the Q0 launch's values survive for them)."""
+thread 0 of the grid's workgroups 0, 1 and its last two stamps s_memtime
+(shader cycles) at: start, tables staged + codeword loaded, pass A done,
+A->B exchange done, pass B done, B->A exchange done, pass A' (and its
+stores) issued.  One k = 512 square; the
+sampled launch is the LAST RS launch of the call (Q2 -> Q3: 1024 workgroups,
+so "last" = 1022/1023, a second-round start)"""
 import ctypes as C
 import os
 import sys
@@ -38,10 +38,10 @@ def main():
         fn(buf)
         v = list(buf)
         rows = []
-        for slot, wg in enumerate((0, 1, 1200, 1201)):
+        for slot, wg in enumerate(("0", "1", "last-1", "last")):
             t = v[8 * slot: 8 * slot + 7]
             d = [t[i + 1] - t[i] for i in range(6)]
-            rows.append(f"  wg {wg:5d}: " + "  ".join(f"{n} {x:6d}" for n, x in zip(names, d)) + f"  total {t[6] - t[0]}")
+            rows.append(f"  wg {wg:>6}: " + "  ".join(f"{n} {x:6d}" for n, x in zip(names, d)) + f"  total {t[6] - t[0]}")
         print(f"rep {rep} (shader cycles)")
         print("\n".join(rows))
 
