@@ -341,10 +341,13 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
     // With the batch split over two streams (n <= 256) each launch holds only
     // its part's lanes, so the lane bound is per launch.
     uint32_t m0 = n_in;
-    if (subtrees && subtree_min_ > 0 && stop >= 2 && n_in % stop == 0) {
+#ifndef CDA_SUBTREE_STOP1
+#define CDA_SUBTREE_STOP1 1   // 0 (A/B build flag): no subtrees where the level launches run down to the roots
+#endif
+    if (subtrees && subtree_min_ > 0 && stop >= (CDA_SUBTREE_STOP1 ? 1u : 2u) && n_in % stop == 0) {
         uint64_t per_node = 0;   // lanes per subtree root per tree
         for (uint32_t i = 0; i < n_forest; i++) per_node += (uint64_t)n * f[i].n_trees;
-        uint32_t sub = stop;
+        uint32_t sub = stop < 2 ? 2 : stop;   // (the roots themselves come from a level launch)
         while (sub < n_in && per_node * sub < subtree_lanes_) sub *= 2;
         bool fits = per_node * sub >= subtree_lanes_ && sub < n_in && n_in / sub >= (uint32_t)subtree_min_;
         const uint32_t slog = fits ? (uint32_t)__builtin_ctz(n_in / sub) : 0;
