@@ -285,6 +285,39 @@ def test_k512_matches_committed_oracle_digest(ctx):
         assert dah.hash().hex() == g[str(i)]["data_root"]
 
 
+def test_k512_batch_of_32_matches_committed_oracle_digest(ctx):
+    """32 k = 512 squares in ONE in-place submission (16 GiB EDS arena): the
+    batch shape whose NMT levels run as a fused subtree launch down to the
+    roots (no tree top) -- squares 0 and 1 of tests/golden/k512.json
+    alternating, every data root and two whole EDSs against the oracle digests."""
+    import json, os
+    import torch
+    from celestia_da import testfactory
+    here = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(here, "golden", "k512.json")))["squares"]
+    k, n = 512, 32
+    W = 2 * k
+    dev = torch.device("cuda", 0)
+    eds = torch.empty((n, W, W, 512), dtype=torch.uint8, device=dev)
+    for i in (0, 1):
+        q0 = torch.from_numpy(testfactory.random_square(k, i)).to(dev).view(k, k, 512)
+        eds[i::2, :k, :k] = q0
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    dr = roots.cpu().numpy()
+    assert [dr[p].tobytes().hex() for p in range(n)] == [g[str(p % 2)]["data_root"] for p in range(n)]
+    for p in (0, n - 1):
+        assert hashlib.sha256(eds[p].cpu().numpy().tobytes()).hexdigest() == g[str(p % 2)]["eds_sha256"], p
+    del eds
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k", [3, 5, 6, 7, 12, 100, 200])
 def test_codec_encode_non_power_of_two(ctx, k):
     """rsmt2d Codec.Encode of a non-power-of-two shard count (klauspost pads
