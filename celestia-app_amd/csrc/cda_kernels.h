@@ -118,7 +118,9 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
 // ONE launch: a lane per (n_in / top)-leaf subtree hashes its nodes in post
 // order (nmt.hip subtree_kernel); roots to out + y*out_sq + (t*top + s)*96,
 // with per-lane stacks behind them (n_trees*top*log2(n_in/top) slots per
-// forest and square in all).  n_in / top a power of two >= 4.
+// forest and square in all); top == 1: the trees' roots to roots /
+// root_slots, as launch_level's last level writes them.  n_in / top a power
+// of two >= 4.
 hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t top, uint32_t n_squares,
                            hipStream_t stream);
 // Every remaining level of up to two forests of n_in (<= 256) nodes per tree

@@ -332,22 +332,22 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
     uint8_t* out = bufA;
     int rc;
     // The first levels as one fused subtree launch (nmt.hip subtree_kernel):
-    // a lane per (n_in / sub)-leaf subtree, sub the smallest node count >=
-    // max(stop, 2) at which the launch holds subtree_lanes_ lanes (default two
-    // waves per SIMD: a lone wave per SIMD issues at ~5.4 cycles per
-    // instruction on this chain, two interleave to the saturated rate); the
-    // levels from sub down to stop then run as per-level launches -- with
-    // stop = 1 (big batches: no tree top) at least the last one, which writes
-    // the roots (config 4: half trees per lane, then one level launch;
-    // levels 15.8 -> 14.2 ms, profiles/r03ab/).  Roots and per-lane stacks
-    // need n_trees * sub * log2(n_in / sub) slots of each forest's output
-    // region.  With the batch split over two streams (n <= 256) each launch
-    // holds only its part's lanes, so the lane bound is per launch.
+    // a lane per (n_in / sub)-leaf subtree, sub the smallest node count >= stop
+    // at which the launch holds subtree_lanes_ lanes (default two waves per
+    // SIMD: a lone wave per SIMD issues at ~5.4 cycles per instruction on this
+    // chain, two interleave to the saturated rate); the levels from sub down
+    // to stop then run as per-level launches.  With stop = 1 (big batches: no
+    // tree top) and sub = 1 a lane hashes a whole tree and the launch writes
+    // the roots itself (config 4: levels 15.8 -> 14.1 ms, profiles/r03ab/,
+    // r03ak/).  Roots and per-lane stacks need n_trees * sub * log2(n_in /
+    // sub) slots of each forest's output region.  With the batch split over
+    // two streams (n <= 256) each launch holds only its part's lanes, so the
+    // lane bound is per launch.
     uint32_t m0 = n_in;
     if (subtrees && subtree_min_ > 0 && stop >= 1 && n_in % stop == 0) {
         uint64_t per_node = 0;   // lanes per subtree root per tree
         for (uint32_t i = 0; i < n_forest; i++) per_node += (uint64_t)n * f[i].n_trees;
-        uint32_t sub = stop < 2 ? 2 : stop;
+        uint32_t sub = stop;
         while (sub < n_in && per_node * sub < subtree_lanes_) sub *= 2;
         bool fits = per_node * sub >= subtree_lanes_ && sub < n_in && n_in / sub >= (uint32_t)subtree_min_;
         const uint32_t slog = fits ? (uint32_t)__builtin_ctz(n_in / sub) : 0;

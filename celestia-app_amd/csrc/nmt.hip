@@ -397,7 +397,16 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
             lvl = nlvl;
             pos = npos;
         }
-        store_slot(out + ((size_t)t * top + s) * kSlot, cur);
+        if (top == 1) {   // whole trees: the roots, as level_kernel's last level writes them
+            if (F.roots) {
+                uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
+#pragma unroll
+                for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(cur[i / 2] >> (16 * (i & 1)));
+            }
+            if (F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, cur);
+        } else {
+            store_slot(out + ((size_t)t * top + s) * kSlot, cur);
+        }
     }
 }
 
