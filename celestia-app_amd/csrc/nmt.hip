@@ -425,25 +425,6 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
 // ---------------------------------------------------------------------------
 constexpr uint32_t kTopThreads = 128;   // parents per workgroup: tpw = 256 / n_in trees x n_in / 2
 
-// Timing probe (tools/top_trace.py; never in the product build): workgroup
-// (0, 0)'s thread 0 stamps s_memtime at the tree top's phase boundaries and
-// at the data-root kernel's levels.
-#ifdef CDA_TOP_TRACE
-__device__ unsigned long long g_top_trace[128];
-__device__ unsigned int g_top_trace_n;
-#define TOP_MARK()                                                                                        \
-    do {                                                                                                  \
-        if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && g_top_trace_n < 127) {             \
-            g_top_trace[g_top_trace_n++] = __builtin_amdgcn_s_memtime();                                  \
-            g_top_trace[g_top_trace_n++] = __builtin_amdgcn_s_memrealtime();                              \
-        }                                                                                                 \
-    } while (0)
-#else
-#define TOP_MARK() \
-    do {           \
-    } while (0)
-#endif
-
 template <bool PAIR>
 __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top_kernel(
     const Forest2 fs, uint32_t n_in, uint32_t tpw, uint32_t* __restrict__ dig, uint32_t n_dig, uint32_t rfc_levels,
@@ -461,7 +442,6 @@ __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top
     const bool writer = !A;                                    // one store per unit
     uint32_t o[kSlotWords];
     uint32_t cur = 0;
-    TOP_MARK();
     for (uint32_t m = n_in; m >= 2; m /= 2) {
         const uint32_t half = m / 2;
         const uint32_t j = u / half, p = u % half;   // tree j of this workgroup, parent p
@@ -552,7 +532,6 @@ __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top
             }
         }
         __syncthreads();
-        TOP_MARK();
         cur ^= 1;
     }
     // unit j < tpw holds tree j's root slot in o
@@ -576,7 +555,6 @@ __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top
             rfc_leaf_u<PAIR>(I, D, A);
         }
     }
-    TOP_MARK();
     if (!dig) return;
     // rfc_levels inner levels over this workgroup's tpw digests (the host only
     // asks for them when every workgroup holds tpw trees): unit u < cnt holds
@@ -600,7 +578,6 @@ __global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top
             rfc_inner_u<PAIR>(a, b, D, A);
         }
         __syncthreads();
-        TOP_MARK();
     }
     if (has && writer && u < cnt) {
         uint4* d = reinterpret_cast<uint4*>(dig + (sq * n_dig + ((blockIdx.x * tpw) >> rfc_levels) + u) * 8);
@@ -852,7 +829,6 @@ __global__ __launch_bounds__(512) void data_root_digest_kernel(const uint32_t* _
     const uint32_t* D = dig + sq * (size_t)n * 8;
     uint32_t* src = hs;
     uint32_t* dst = hs + (n / 2) * 8;
-    TOP_MARK();
     for (uint32_t m = n / 2; m >= 1; m >>= 1) {
         const uint32_t* in = m == n / 2 ? D : src;
         uint32_t* out = m == n / 2 ? src : dst;
@@ -863,7 +839,6 @@ __global__ __launch_bounds__(512) void data_root_digest_kernel(const uint32_t* _
         else
             data_root_level<false>(in, out, m);
         __syncthreads();
-        TOP_MARK();
         if (m != n / 2) {
             uint32_t* t = src; src = dst; dst = t;
         }
@@ -973,19 +948,6 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
                        hash_lds(reinterpret_cast<const void*>(level_kernel)), s, fs, n_in, nbx, n, nblocks);
     return hipGetLastError();
 }
-
-#ifdef CDA_TOP_TRACE
-extern "C" int cda_debug_top_trace(unsigned long long* out, unsigned int max_n) {
-    unsigned int n = 0;
-    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_top_trace_n), sizeof n) != hipSuccess) return -1;
-    if (n > max_n) n = max_n;
-    if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_top_trace), n * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    const unsigned int zero = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_top_trace_n), &zero, sizeof zero) != hipSuccess) return -1;
-    return (int)n;
-}
-#endif
 
 hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t top, uint32_t n, hipStream_t s) {
     if (n_forest < 1 || n_forest > 2 || top < 1 || n_in % top) return hipErrorInvalidValue;

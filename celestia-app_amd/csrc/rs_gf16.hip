@@ -701,30 +701,10 @@ __device__ __forceinline__ void stage_record(uint32_t* dst, const uint32_t* __re
     for (int q = 0; q < 5; q++) d[q] = s[q];
 }
 
-// Timing probe (tools/rs16_phases.py; never in the product build; outputs
-// unchanged): thread 0 of four sampled workgroups (the grid's first two and
-// last two) stamps s_memtime at the kernel's phase boundaries.
-#ifdef CDA_RS16_PHASES
-__device__ unsigned long long g_rs16_phase[4][8];
-#define RS16_MARK(i)                                                                                      \
-    do {                                                                                                  \
-        const uint32_t b_ = blockIdx.x;                                                                   \
-        const uint32_t e_ = gridDim.x;                                                                    \
-        const int slot_ = b_ == 0 ? 0 : b_ == 1 ? 1 : b_ == e_ - 2 ? 2 : b_ == e_ - 1 ? 3 : -1;           \
-        if (slot_ >= 0 && blockIdx.y == 0 && threadIdx.x == 0)                                            \
-            g_rs16_phase[slot_][i] = __builtin_amdgcn_s_memtime();                                        \
-    } while (0)
-#else
-#define RS16_MARK(i) \
-    do {             \
-    } while (0)
-#endif
-
 template <int K>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs16_half_kernel(
     const uint32_t* __restrict__ tab, const RsJob job) {
     static_assert(CDA_RS16_LDS_A, "the half-width kernel reads passes A / A' tables from LDS");
-    RS16_MARK(0);
     rs_err_init(job);
     extern __shared__ uint32_t X[];
     constexpr int S = K / 16;      // shards per virtual wave in pass A
@@ -851,13 +831,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         stage_record(X + kTPB + tid * kTbStride, tab, tid < 16 ? K - 1 + S * tid : S * (tid - 16) - 1);
     __syncthreads();
 #endif
-    RS16_MARK(1);
     if (c0 != kNoCopy) {
         sfor<0, S, 1>([&](auto jj) { st(E, c0 + (wb + jj.value) * g.cpy_sh, lcpy, lo[jj.value], hi[jj.value]); });
     }
     layers_regs_lds<S, true, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d); }, NoFin{},
                                        kPlaneA);
-    RS16_MARK(2);
     // once every wave is past pass A (the exchange's first barrier), the
     // transform records are restaged with the FFT's constants 0..K-1 for pass
     // A'; the B -> A exchange's first barrier publishes them
@@ -866,7 +844,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     // the DMA's address arithmetic spilled 34 VGPRs)
     xchg_a_to_b([] {});
     dma_records(0);
-    RS16_MARK(3);
 #else
     xchg_a_to_b([] {});
     for (uint32_t i = tid; i < K; i += 512) stage_record(X + kTA + i * kTbStride, tab, i);
@@ -901,14 +878,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             });
         });
     }
-    RS16_MARK(4);
     xchg_b_to_a();
-    RS16_MARK(5);
     // ---------------- pass A': FFT d = S/2 .. 1, write parity -------------
     auto store_j = [&](auto jj) { st(E, d0 + (wb + jj.value) * ds, ldst, lo[jj.value], hi[jj.value]); };
     layers_regs_lds<S, false, kRs16Dfs>(lo, hi, TBv, [](int gg, int d) { return (uint32_t)(gg + d - 1); }, store_j,
                                         kPlaneA);
-    RS16_MARK(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -1036,12 +1010,6 @@ hipError_t launch_cw(const Gf16Dev& t, const RsJob& j, uint32_t n, hipStream_t s
 
 
 hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s);
-
-#ifdef CDA_RS16_PHASES
-extern "C" int cda_debug_rs16_phases(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rs16_phase), sizeof(g_rs16_phase)) == hipSuccess ? 32 : -1;
-}
-#endif
 
 hipError_t launch_rs(const RsJob& j, uint32_t k, uint32_t n, const Gf16Dev& t, hipStream_t s) {
     if (k == 0 || (k & (k - 1))) return hipErrorInvalidValue;

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Phase timeline of rs16_half_kernel<512> from a -DCDA_RS16_PHASES build
-(tools/build_variant.sh rs16ph -DCDA_RS16_PHASES; run with CDA_LIB=<that>):
+"""Phase timeline of rs16_half_kernel<512> from a timing-probe build
+(PATCH=tools/probes/rs16_phases.patch tools/build_variant.sh rs16ph
+-DCDA_RS16_PHASES; run with CDA_LIB=<that>):
 thread 0 of the grid's workgroups 0, 1 and its last two stamps s_memtime
 (shader cycles) at: start, tables staged + codeword loaded, pass A done,
 A->B exchange done, pass B done, B->A exchange done, pass A' (and its

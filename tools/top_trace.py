@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase timeline of the latency chain's tree top and data root (configs 2
-and 3) from a -DCDA_TOP_TRACE build (tools/build_variant.sh toptrace
--DCDA_TOP_TRACE; run with CDA_LIB=<that>/libcda.so): workgroup (0, 0)'s thread 0
+and 3) from a timing-probe build (PATCH=tools/probes/top_trace.patch
+tools/build_variant.sh toptrace -DCDA_TOP_TRACE; run with CDA_LIB=<that>/libcda.so): workgroup (0, 0)'s thread 0
 stamps s_memtime / s_memrealtime (100 MHz) at every level boundary of
 tree_top_kernel and data_root_digest_kernel.  Prints per-phase deltas."""
 import ctypes as C
