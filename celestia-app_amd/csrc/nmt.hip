@@ -319,13 +319,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
 // top_fuse_nodes, so lanes = n * 2W * top >= 65 536).  A lone wave issues an
 // instruction every ~4.25 cycles, about the rate of a SIMD saturated with the
 // same mixed stream, so these chains run at the wide
-// launches' compression rate without their tails.  The operands of the next
-// iteration (a leaf pair, or a stored left sibling) are loaded one iteration
-// ahead; pending left siblings go to a per-lane stack in the forest's output
-// buffer behind the subtree roots (written and read by the same lane).  A
-// wave is 64 consecutive trees of one subtree index, so the parity
-// mid-state branch of hash_node stays uniform.
+// launches' compression rate without their tails.  Each iteration loads its
+// operands (a leaf pair, or a stored left sibling) at use: 141 VGPRs, three
+// waves per SIMD, whose loads hide behind each other's hashing -- against
+// round 3's first form, which loaded them one iteration ahead as raw words
+// (189 VGPRs, two waves per SIMD; CDA_SUBTREE_NOPF=0 builds it): config 4's
+// levels 14.06 -> 13.90 ms, one k = 512 square unchanged (profiles/r03ar/).
+// Pending left siblings go to a per-lane stack in the forest's output buffer
+// behind the subtree roots (written and read by the same lane).  A wave is
+// 64 consecutive trees of one subtree index, so the parity mid-state branch
+// of hash_node stays uniform.
 // ---------------------------------------------------------------------------
+#ifndef CDA_SUBTREE_NOPF
+#define CDA_SUBTREE_NOPF 1
+#endif
 __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx,
                                                       uint32_t nsq, uint32_t nblocks) {
     const uint32_t S = 1u << slog;
@@ -363,6 +370,32 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
                 w[4 * i + 2] = bswap32(q[i].z); w[4 * i + 3] = bswap32(q[i].w);
             }
         };
+#if CDA_SUBTREE_NOPF
+        (void)nL; (void)nR;
+        uint32_t j = 0, lvl = 0, pos = 0;
+#pragma unroll 1
+        for (uint32_t it = 0; it + 1 < S; it++) {
+            const bool merge = it > 0 && (pos & 1);
+            const uint8_t* pa = merge ? stack_slot(lvl) : in + (size_t)(2 * j) * leaf_step;
+            const uint8_t* pb = merge ? pa : in + (size_t)(2 * j + 1) * leaf_step;
+            uint4 a[6], b[6];
+            load_raw(pa, a);
+            load_raw(pb, b);
+            uint32_t L[kSlotWords], R[kSlotWords];
+            be(a, L);
+            be(b, R);
+            if (merge) {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) R[i] = bswap32(cur[i]);
+            }
+            const uint32_t nlvl = merge ? lvl + 1 : 1u, npos = merge ? pos >> 1 : j;
+            if (!merge) j++;
+            hash_node(L, R, cur);
+            if (!(npos & 1) && nlvl < slog) store_slot(stack_slot(nlvl), cur);
+            lvl = nlvl;
+            pos = npos;
+        }
+#else
         load_raw(in, nL);
         load_raw(in + leaf_step, nR);
         uint32_t j = 0;               // next unconsumed leaf pair (pair 0 is in nL / nR)
@@ -397,6 +430,7 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
             lvl = nlvl;
             pos = npos;
         }
+#endif
         if (top == 1) {   // whole trees: the roots, as level_kernel's last level writes them
             if (F.roots) {
                 uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
