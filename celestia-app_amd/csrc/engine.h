@@ -242,7 +242,7 @@ class Engine {
                     uint64_t buf_sq, const uint64_t* out_off, hipStream_t s, uint32_t stop = 1,
                     bool subtrees = false);
     int subtree_min_ = 8;   // CDA_SUBTREE: fused subtree levels of >= this many leaves (0 = off)
-    uint64_t subtree_lanes_ = 131072;   // CDA_SUBTREE_LANES: lanes a subtree launch must hold
+    uint64_t subtree_lanes_ = 0;   // CDA_SUBTREE_LANES: lanes a subtree launch must hold (0 = by tree size)
     uint32_t top_fuse_nodes(uint32_t W, uint32_t n) const;
     int top_fuse_ = -1;   // CDA_TOP_FUSE (tuning / A-B): -1 auto, 0 off, N = nodes per tree
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,

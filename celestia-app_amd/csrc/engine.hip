@@ -333,7 +333,7 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
     int rc;
     // The first levels as one fused subtree launch (nmt.hip subtree_kernel):
     // a lane per (n_in / sub)-leaf subtree, sub the smallest node count >= stop
-    // at which the launch holds subtree_lanes_ lanes (default two waves per
+    // at which the launch holds `want` lanes (default two waves per
     // SIMD: a lone wave per SIMD issues at ~5.4 cycles per instruction on this
     // chain, two interleave to the saturated rate); the levels from sub down
     // to stop then run as per-level launches.  With stop = 1 (big batches: no
@@ -348,8 +348,12 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
         uint64_t per_node = 0;   // lanes per subtree root per tree
         for (uint32_t i = 0; i < n_forest; i++) per_node += (uint64_t)n * f[i].n_trees;
         uint32_t sub = stop;
-        while (sub < n_in && per_node * sub < subtree_lanes_) sub *= 2;
-        bool fits = per_node * sub >= subtree_lanes_ && sub < n_in && n_in / sub >= (uint32_t)subtree_min_;
+        // default target: 131072 lanes (two waves per SIMD); 262144 for trees
+        // of >= 1024 leaves (k >= 512: one k = 512 square 1.096 -> 1.087 ms,
+        // 8- instead of 16-leaf subtrees; profiles/r03at/)
+        const uint64_t want = subtree_lanes_ ? subtree_lanes_ : n_in >= 1024 ? 262144u : 131072u;
+        while (sub < n_in && per_node * sub < want) sub *= 2;
+        bool fits = per_node * sub >= want && sub < n_in && n_in / sub >= (uint32_t)subtree_min_;
         const uint32_t slog = fits ? (uint32_t)__builtin_ctz(n_in / sub) : 0;
         for (uint32_t i = 0; i < n_forest && fits; i++) {
             const uint64_t need = (uint64_t)f[i].n_trees * sub * slog * kSlot;
