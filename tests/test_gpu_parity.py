@@ -318,6 +318,46 @@ def test_k512_batch_of_32_matches_committed_oracle_digest(ctx):
     torch.cuda.empty_cache()
 
 
+def test_k32_batch_of_1024_whole_tree_subtrees_match_single_squares(ctx):
+    """1024 k = 32 squares in one in-place submission -- the shape whose NMT
+    levels run as ONE subtree launch of whole 64-leaf trees that writes the
+    roots itself (no tree top) -- against the same squares extended one at a
+    time (tree-top path) and, for two of them, the C oracle."""
+    import torch
+    from celestia_da import testfactory
+    k, n, distinct = 32, 1024, 64
+    W = 2 * k
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ods = [torch.from_numpy(testfactory.random_square(k, i)).to(dev).view(k, k, 512) for i in range(distinct)]
+
+    def run(m, fill):
+        eds = torch.zeros((m, W, W, 512), dtype=torch.uint8, device=dev)
+        for p in range(m):
+            eds[p, :k, :k] = fill(p)
+        rows = torch.empty(m, W * 90, dtype=torch.uint8, device=dev)
+        cols = torch.empty(m, W * 90, dtype=torch.uint8, device=dev)
+        roots = torch.empty(m, 32, dtype=torch.uint8, device=dev)
+        status = torch.empty(m, dtype=torch.int32, device=dev)
+        ctx.extend_dah_inplace_device(k, m, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                      status.data_ptr(), s)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == 0).all()
+        return roots.cpu().numpy(), rows.cpu().numpy(), cols.cpu().numpy()
+
+    batch = run(n, lambda p: ods[p % distinct])
+    for i in range(distinct):
+        one = run(1, lambda p: ods[i])
+        for p in range(i, n, distinct):
+            assert batch[0][p].tobytes() == one[0][0].tobytes(), (i, p)
+            assert batch[1][p].tobytes() == one[1][0].tobytes(), (i, p)
+            assert batch[2][p].tobytes() == one[2][0].tobytes(), (i, p)
+    for i in (0, distinct - 1):
+        _, wrows, wcols, wroot = coracle.extend_dah(testfactory.random_square(k, i))
+        assert batch[0][i].tobytes() == wroot, i
+        assert batch[1][i].tobytes() == wrows.tobytes() and batch[2][i].tobytes() == wcols.tobytes(), i
+
+
 @pytest.mark.parametrize("k", [3, 5, 6, 7, 12, 100, 200])
 def test_codec_encode_non_power_of_two(ctx, k):
     """rsmt2d Codec.Encode of a non-power-of-two shard count (klauspost pads
