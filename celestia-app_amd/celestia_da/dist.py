@@ -159,6 +159,7 @@ def extend_dah_split_rccl(ctx, ods_rows, k: int, rank: int, world: int, stream=N
     ctx.extend_dah_split(ods_rows.data_ptr(), k, block.data_ptr(), rows.data_ptr() if rank == 0 else None,
                          cols.data_ptr() if rank == 0 else None, root.data_ptr() if rank == 0 else None,
                          err.data_ptr(), stream)
+    # rank 0 raises (CDA_ERR_DEVICE) when a peer failed: the reduced word is then 0
     result = (rows, cols, root, err.to(torch.int64) & 0xFFFFFFFF) if rank == 0 else None
     return block, result
 

@@ -61,6 +61,8 @@ constexpr uint32_t kGf16TabWords = 24;
 // Leopard encode of every codeword of `job` for n_squares squares; k data
 // shards of 512 B per codeword (GF(2^8) for k <= 128, GF(2^16) above).
 hipError_t launch_rs(const RsJob& job, uint32_t k, uint32_t n_squares, const Gf16Dev& gf16, hipStream_t stream);
+// Bitsliced GF(2^16) encode of every codeword of `job` (k = 256 or 512).
+hipError_t launch_rs16_bs(const RsJob& job, uint32_t k, uint32_t n_squares, hipStream_t stream);
 // rsmt2d Codec.Encode of n_code contiguous codewords of k shards x len bytes.
 hipError_t launch_rs8_flat(const uint8_t* data, uint8_t* parity, uint32_t k, uint32_t len, uint32_t n_code,
                            hipStream_t stream);

@@ -15,8 +15,10 @@
 // pkg/da/data_availability_header.go:44-75.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -80,21 +82,47 @@ int comm_unique_id(uint8_t* id) {
 int Engine::comm_init(int rank, int world, const uint8_t* id) {
     if (world < 1 || rank < 0 || rank >= world) return fail(CDA_ERR_INVALID, "bad rank / world size");
     comm_destroy();
+    // the agreement round's words (split_extend_dah): preset 0 and 1, so the
+    // all-reduce needs no copy that could fail before it
+    int rc;
+    if ((rc = check(comm_flag_.ensure(16), "hipMalloc agreement words"))) return rc;
+    const int32_t preset[4] = {0, 1, 0, 0};
+    if ((rc = check(hipMemcpy(comm_flag_.ptr, preset, sizeof preset, hipMemcpyHostToDevice), "hipMemcpy agreement words")))
+        return rc;
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof uid);
     ncclComm_t c = nullptr;
     ncclResult_t r = ncclCommInitRank(&c, world, uid, rank);
     if (r != ncclSuccess) return fail(CDA_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    comm_ = c;
+    {
+        std::lock_guard<std::mutex> g(comm_mu_);
+        comm_ = c;
+    }
     rank_ = rank;
     world_ = world;
     comm_k_ = 0;
     return CDA_OK;
 }
 
-// comm_ is swapped out atomically: cda_comm_abort may run on a watchdog
-// thread while another thread holds the context inside a collective.
-void* Engine::take_comm() { return __atomic_exchange_n(&comm_, nullptr, __ATOMIC_ACQ_REL); }
+// cda_comm_abort may run on a watchdog thread while another thread is inside
+// split_extend_dah.  comm_ changes only under comm_mu_, every RCCL post (group
+// start, send / recv / reduce) runs under it after re-reading comm_, and the
+// blocking steps (ncclGroupEnd -- it may wait for peers while it connects --
+// and stream syncs) run unlocked and re-read comm_ when they return.  So a
+// post never sees a freed communicator, and an abort during a blocking step
+// releases it (ncclCommAbort stops the queued collectives) and the call
+// returns CDA_ERR_COMM without touching the communicator again.
+void* Engine::take_comm() {
+    std::lock_guard<std::mutex> g(comm_mu_);
+    void* c = comm_;
+    comm_ = nullptr;
+    return c;
+}
+
+bool Engine::comm_alive() {
+    std::lock_guard<std::mutex> g(comm_mu_);
+    return comm_ != nullptr;
+}
 
 void Engine::comm_destroy() {
     if (void* c = take_comm()) (void)ncclCommDestroy(static_cast<ncclComm_t>(c));
@@ -122,33 +150,58 @@ int Engine::comm_abort() {
     return CDA_OK;
 }
 
+static int aborted(Engine& e, const char* what) {
+    return e.fail(CDA_ERR_COMM, std::string(what) + ": the communicator was aborted during the call (cda_comm_abort)");
+}
+
+// One RCCL group: the posts under comm_mu_, ncclGroupEnd unlocked.  A group
+// is always closed, even after a failed post.
+int Engine::comm_group(const char* what, const std::function<int(void*)>& post) {
+    ncclResult_t first;
+    bool opened = false;
+    {
+        std::lock_guard<std::mutex> g(comm_mu_);
+        if (!comm_) return aborted(*this, what);
+        first = ncclGroupStart();
+        if (first == ncclSuccess) {
+            opened = true;
+            first = static_cast<ncclResult_t>(post(comm_));
+        }
+    }
+    const ncclResult_t end = opened ? ncclGroupEnd() : ncclSuccess;
+    if (!comm_alive()) return aborted(*this, what);
+    if (first != ncclSuccess) return comm_fail(what, first);
+    if (end != ncclSuccess) return comm_fail(what, end);
+    return CDA_OK;
+}
+
 // Config 5 on this rank.  Error discipline (every rank must leave every
 // collective it entered, or its peers block forever):
 //   * checks that depend only on k and the world size fail on every rank alike
 //     before any collective;
 //   * scratch is allocated when k changes, followed by one agreement
-//     all-reduce (MIN of an ok flag, read back on the host): if any rank could
-//     not allocate, every rank returns CDA_ERR_OOM and the communicator stays
+//     all-reduce (MIN of an ok flag -- one of two preset device words, so no
+//     copy precedes it -- read back on the host): if any rank could not
+//     allocate, every rank returns CDA_ERR_OOM and the communicator stays
 //     usable;
 //   * a local failure after that (a kernel launch, bad per-rank buffers) does
 //     not return early: the rank stops its own compute, poisons its push-order
 //     word with 0 (never a valid violation word: positions start at 1), takes
-//     part in the remaining collectives and returns its error at the end; rank
-//     0 then finds 0 in the MIN-reduced word and skips the combine;
+//     part in the remaining collectives and returns its error at the end;
+//     rank 0 reads the MIN-reduced word back, and when it is 0 (a peer
+//     failed) skips the combine and returns CDA_ERR_DEVICE;
 //   * an RCCL call that fails closes its group (ncclGroupEnd), aborts the
-//     communicator and returns CDA_ERR_COMM.
+//     communicator and returns CDA_ERR_COMM; so does an abort by another
+//     thread (cda_comm_abort) while the call waits in a collective.
 int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_block, uint8_t* d_row_roots,
                              uint8_t* d_col_roots, uint8_t* d_root, uint32_t* d_err, hipStream_t s) {
-    if (!comm_) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
+    if (!comm_alive()) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
     const uint32_t G = (uint32_t)world_, W = 2 * k;
     if (k == 0 || (k & (k - 1)) || (G & (G - 1)) || k % G || k > 1024)
         return fail(CDA_ERR_INVALID, "world size must divide k (a power of two <= 1024)");
     const uint32_t R = k / G, C = W / G;
     const size_t piece = (size_t)R * C * kShare;   // one rank pair's all-to-all block
     const size_t own = (size_t)(C + W) * kSlot, all = (size_t)G * (C + W) * kSlot;
-    ncclComm_t comm = static_cast<ncclComm_t>(__atomic_load_n(&comm_, __ATOMIC_ACQUIRE));
-    if (!comm) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
-    ncclResult_t r;
     int rc;
     // -- scratch + agreement (only when k changes; k is the same on every rank) --
     if (comm_k_ != k) {
@@ -162,14 +215,20 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
         if (ok && leaf_.ensure((size_t)W * C * kSlot) != hipSuccess) ok = 0;
         if (ok && lvl_.ensure((size_t)W * C * kSlot) != hipSuccess) ok = 0;
         (void)hipGetLastError();
-        if ((rc = check(comm_flag_.ensure(4), "hipMalloc agreement word"))) return rc;
-        int32_t* d_ok = comm_flag_.as<int32_t>();
-        int32_t h_ok = ok;
-        if ((rc = check(hipMemcpyAsync(d_ok, &h_ok, 4, hipMemcpyHostToDevice, s), "H2D agreement word"))) return rc;
-        if ((r = ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, comm, s)) != ncclSuccess)
-            return comm_fail("ncclAllReduce (allocation agreement)", r);
-        if ((rc = check(hipMemcpyAsync(&h_ok, d_ok, 4, hipMemcpyDeviceToHost, s), "D2H agreement word"))) return rc;
-        if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+        int32_t* words = comm_flag_.as<int32_t>();
+        if ((rc = comm_group("ncclAllReduce (allocation agreement)", [&](void* c) {
+                 return (int)ncclAllReduce(words + (ok ? 1 : 0), words + 2, 1, ncclInt32, ncclMin,
+                                           static_cast<ncclComm_t>(c), s);
+             })))
+            return rc;
+        int32_t h_ok = 0;
+        if ((rc = check(hipMemcpyAsync(&h_ok, words + 2, 4, hipMemcpyDeviceToHost, s), "D2H agreement word"))) return rc;
+        if (comm_fault("stall")) {   // tests: wait here as if a peer never arrived, until aborted
+            for (int i = 0; i < 30000 && comm_alive(); i++) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        const hipError_t se = hipStreamSynchronize(s);
+        if (!comm_alive()) return aborted(*this, "allocation agreement");
+        if ((rc = check(se, "hipStreamSynchronize"))) return rc;
         if (!h_ok)
             return fail(CDA_ERR_OOM, ok ? "a peer rank could not allocate its split scratch"
                                         : "split scratch allocation failed on this rank");
@@ -204,14 +263,6 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
         local_fail(e, last_error());
         return hipMemsetAsync(err, 0x00, 4, s) == hipSuccess;
     };
-    auto grouped = [&](const char* what, auto&& post) -> int {
-        if ((r = ncclGroupStart()) != ncclSuccess) return comm_fail(what, r);
-        const ncclResult_t first = post();
-        const ncclResult_t end = ncclGroupEnd();   // always closed, even after a failed post
-        if (first != ncclSuccess) return comm_fail(what, first);
-        if (end != ncclSuccess) return comm_fail(what, end);
-        return CDA_OK;
-    };
     if (G == 1) {
         // one rank: the row block IS rows 0..k-1 of the (whole) column block
         if (!step([&] { return enqueue_split_rows_send(d_rows, k, R, 0, 1, block, err, s); }))
@@ -224,14 +275,15 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
             return comm_fail("poison", ncclUnhandledCudaError);
         // 2. all-to-all: piece h goes to rank h; rank g's piece lands at rows
         //    g*R..g*R+R-1 of the column block
-        if ((rc = grouped("all-to-all", [&]() -> ncclResult_t {
-                 if (comm_fault("a2a")) return ncclInternalError;
+        if ((rc = comm_group("all-to-all", [&](void* cv) -> int {
+                 if (comm_fault("a2a")) return (int)ncclInternalError;
+                 ncclComm_t comm = static_cast<ncclComm_t>(cv);
                  for (uint32_t h = 0; h < G; h++) {
                      ncclResult_t q = ncclSend(split_send_.as<uint8_t>() + h * piece, piece, ncclUint8, (int)h, comm, s);
-                     if (q != ncclSuccess) return q;
-                     if ((q = ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s)) != ncclSuccess) return q;
+                     if (q != ncclSuccess) return (int)q;
+                     if ((q = ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s)) != ncclSuccess) return (int)q;
                  }
-                 return ncclSuccess;
+                 return (int)ncclSuccess;
              })))
             return rc;
     }
@@ -241,31 +293,45 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
             return enqueue_split_cols(block, k, C, (uint32_t)rank_ * C, col_slots, row_sub, err, s);
         }))
         return comm_fail("poison", ncclUnhandledCudaError);
+    if (comm_fault("peer") && hipMemsetAsync(err, 0x00, 4, s) != hipSuccess)   // tests: as if a peer had failed
+        return comm_fail("poison", ncclUnhandledCudaError);
     // 4. gather the slots on rank 0 and reduce the push-order word
-    if ((rc = grouped("gather", [&]() -> ncclResult_t {
-             if (comm_fault("gather")) return ncclInternalError;
+    if ((rc = comm_group("gather", [&](void* cv) -> int {
+             if (comm_fault("gather")) return (int)ncclInternalError;
+             ncclComm_t comm = static_cast<ncclComm_t>(cv);
              ncclResult_t q;
              if (rank_ == 0) {
                  for (uint32_t h = 0; h < G; h++) {
                      if ((q = ncclRecv(g_sub + (size_t)h * W * kSlot, (size_t)W * kSlot, ncclUint8, (int)h, comm, s)) !=
                          ncclSuccess)
-                         return q;
+                         return (int)q;
                      if ((q = ncclRecv(g_col + (size_t)h * C * kSlot, (size_t)C * kSlot, ncclUint8, (int)h, comm, s)) !=
                          ncclSuccess)
-                         return q;
+                         return (int)q;
                  }
              }
-             if ((q = ncclSend(row_sub, (size_t)W * kSlot, ncclUint8, 0, comm, s)) != ncclSuccess) return q;
-             return ncclSend(col_slots, (size_t)C * kSlot, ncclUint8, 0, comm, s);
+             if ((q = ncclSend(row_sub, (size_t)W * kSlot, ncclUint8, 0, comm, s)) != ncclSuccess) return (int)q;
+             return (int)ncclSend(col_slots, (size_t)C * kSlot, ncclUint8, 0, comm, s);
          })))
         return rc;
-    if ((r = ncclReduce(err, err, 1, ncclUint32, ncclMin, 0, comm, s)) != ncclSuccess) return comm_fail("ncclReduce", r);
+    if ((rc = comm_group("ncclReduce", [&](void* cv) {
+             return (int)ncclReduce(err, err, 1, ncclUint32, ncclMin, 0, static_cast<ncclComm_t>(cv), s);
+         })))
+        return rc;
     if (local != CDA_OK) return fail(local, local_msg);
-    // 5. rank 0: top log2(G) levels of every row tree, roots, data root (a
-    //    peer that failed left 0 in the reduced word: the combine still runs on
-    //    whatever arrived, and the caller sees d_err == 0)
-    if (rank_ == 0) return enqueue_split_combine(g_sub, G, k, g_col, d_row_roots, d_col_roots, d_root, s);
-    return CDA_OK;
+    if (rank_ != 0) return CDA_OK;
+    // 5. rank 0: a peer that failed left 0 in the reduced word -- nothing valid
+    //    to combine; otherwise the top log2(G) levels of every row tree, the
+    //    roots and the data root
+    uint32_t word = 0;
+    if ((rc = check(hipMemcpyAsync(&word, err, 4, hipMemcpyDeviceToHost, s), "D2H push-order word"))) return rc;
+    const hipError_t se = hipStreamSynchronize(s);
+    if (!comm_alive()) return aborted(*this, "ncclReduce");
+    if ((rc = check(se, "hipStreamSynchronize"))) return rc;
+    if (word == 0)
+        return fail(CDA_ERR_DEVICE,
+                    "a peer rank failed its local stage (MIN-reduced push-order word 0): roots not written");
+    return enqueue_split_combine(g_sub, G, k, g_col, d_row_roots, d_col_roots, d_root, s);
 }
 
 }  // namespace cda

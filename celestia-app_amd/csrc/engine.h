@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -28,6 +29,10 @@ struct HostPin {
     hipStream_t s0, s1;
     HostPin(bool on, const void* q, size_t bytes, hipStream_t a, hipStream_t b) : s0(a), s1(b) {
         if (!on || !q || !bytes) return;
+        // already page-locked (hipHostMalloc / registered by the caller): nothing to do
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, q) == hipSuccess && attr.type == hipMemoryTypeHost) return;
+        (void)hipGetLastError();
         if (hipHostRegister(const_cast<void*>(q), bytes, hipHostRegisterDefault) == hipSuccess)
             p = const_cast<void*>(q);
         else
@@ -50,9 +55,16 @@ hipError_t launch_share_writer(const square::Segment* segs, uint32_t n_segs, con
                                const uint8_t* compact, const uint8_t* txs, uint8_t* ods, uint32_t n_shares,
                                hipStream_t s);
 
+// Device scratch that only grows.  Inside a context call (between
+// Engine::order_begin and order_end) growth is stream-ordered: the old buffer
+// is released with hipFreeAsync on the call's stream -- which already waits
+// for every earlier call of the context -- and the new one comes from
+// hipMallocAsync on it, so device entry points stay enqueue-only (no device
+// synchronisation).  Outside a call (context set-up) plain hipMalloc / hipFree.
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
+    bool pooled = false;   // allocated by hipMallocAsync
     hipError_t ensure(size_t n);
     void release();
     template <class T>
@@ -267,7 +279,19 @@ class Engine {
     // copy_out_ while stream_ hashes (ev_rs_: RS done, ev_out_: copies done)
     hipStream_t copy_out_ = nullptr;
     hipEvent_t ev_rs_ = nullptr, ev_out_ = nullptr;
-    int enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds);
+    int enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
+                           hipEvent_t ready, hipEvent_t done);
+    // Big host-buffer batches (host_extend_dah, n > 2 chunks): chunks of
+    // squares through a ring of kPipeSlots device slots, H2D on copy_in_,
+    // extension + hashing on stream_, parity D2H on copy_out_, so chunk i+1
+    // goes up while chunk i computes and chunk i-1 comes down.
+    static constexpr uint32_t kPipeSlots = 3;
+    hipStream_t copy_in_ = nullptr;
+    hipEvent_t pipe_in_[kPipeSlots] = {}, pipe_rs_[kPipeSlots] = {}, pipe_d2h_[kPipeSlots] = {},
+               pipe_comp_[kPipeSlots] = {};
+    uint32_t host_pipe_chunk_ = 0;   // CDA_HOST_PIPE_CHUNK: squares per chunk (0 = auto: ~256 MiB of ODS)
+    int host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
+                      uint8_t* roots, int32_t* status, uint32_t chunk);
     static void copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds);
     hipEvent_t order_ev_ = nullptr;   // end of the last call's GPU work
     bool order_used_ = false;
@@ -332,12 +356,22 @@ class Engine {
     DevBuf rs_pad_;   // Codec.Encode of a non-power-of-two shard count
     // config 5 in the library: RCCL communicator (ncclComm_t), row block,
     // send buffer, column block, slots
+    // comm_mu_ guards comm_ and every non-blocking RCCL post; cda_comm_abort
+    // takes comm_ under it, so no post touches an aborted communicator, while
+    // the blocking calls (ncclGroupEnd, stream syncs) run unlocked and re-read
+    // comm_ after they return (comm.hip).
     void* comm_ = nullptr;
+    std::mutex comm_mu_;
     int rank_ = 0, world_ = 0;
     uint32_t comm_k_ = 0;   // k whose split scratch every rank agreed on (0 = none yet)
+    // comm_flag_: the agreement round's words, allocated by comm_init: [0] = 0,
+    // [1] = 1 (the all-reduce sends one of them, so nothing can fail before
+    // it), [2] = the MIN result
     DevBuf split_blk_, split_send_, split_col_, split_slots_, comm_flag_;
     int comm_fail(const char* what, int nccl_result);
-    void* take_comm();   // abort + release the communicator, CDA_ERR_COMM
+    void* take_comm();   // comm_ = nullptr under comm_mu_; returns the old value
+    bool comm_alive();
+    int comm_group(const char* what, const std::function<int(void*)>& post);
     int build_trees(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t n_trees, uint32_t square_size,
                     const uint32_t* axis, std::vector<uint64_t>* level_off, std::vector<uint32_t>* err_out);
     int tree_order_error(const uint8_t* cells, uint32_t cell_len, uint32_t n_cells, uint32_t square_size,

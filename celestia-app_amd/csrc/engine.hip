@@ -23,30 +23,56 @@
 
 namespace cda {
 
+// the stream of the context call running on this thread (order_begin / order_end)
+static thread_local bool tl_in_call = false;
+static thread_local hipStream_t tl_call_stream = nullptr;
+
 hipError_t DevBuf::ensure(size_t n) {
     if (n <= bytes && ptr) return hipSuccess;
-    // Growing: queued work (any stream) may still read the old buffer, so the
-    // device drains before it is freed (hipFree synchronises the device in HIP
-    // anyway).  Buffers only grow, so this happens a handful of times per
-    // context; a caller that needs every device entry point to stay
-    // enqueue-only sizes the scratch once up front (cda_reserve).
-    if (ptr) (void)hipDeviceSynchronize();
+    const size_t want = n < 256 ? 256 : n;
+    if (tl_in_call) {
+        // Growing inside a call: work queued earlier (this call's, or an
+        // earlier call's -- the call stream waits for those) may still read the
+        // old buffer, so it is freed in stream order after that work; no sync.
+        if (ptr) {
+            if (pooled) (void)hipFreeAsync(ptr, tl_call_stream);
+            else (void)hipFree(ptr);   // a set-up allocation (never regrown in practice)
+        }
+        ptr = nullptr;
+        bytes = 0;
+        hipError_t e = hipMallocAsync(&ptr, want, tl_call_stream);
+        if (e != hipSuccess) {
+            ptr = nullptr;
+            return e;
+        }
+        pooled = true;
+        bytes = want;
+        return hipSuccess;
+    }
     release();
-    size_t want = n < 256 ? 256 : n;
     hipError_t e = hipMalloc(&ptr, want);
     if (e != hipSuccess) {
         ptr = nullptr;
         bytes = 0;
         return e;
     }
+    pooled = false;
     bytes = want;
     return hipSuccess;
 }
 
 void DevBuf::release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) {
+        if (pooled) {
+            (void)hipFreeAsync(ptr, nullptr);
+            (void)hipStreamSynchronize(nullptr);
+        } else {
+            (void)hipFree(ptr);
+        }
+    }
     ptr = nullptr;
     bytes = 0;
+    pooled = false;
 }
 
 Engine::Engine(int device) : device_(device) {}
@@ -75,6 +101,10 @@ Engine::~Engine() {
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (ev_rs_) (void)hipEventDestroy(ev_rs_);
     if (ev_out_) (void)hipEventDestroy(ev_out_);
+    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
+        for (uint32_t i = 0; i < kPipeSlots; i++)
+            if (e[i]) (void)hipEventDestroy(e[i]);
+    if (copy_in_) (void)hipStreamDestroy(copy_in_);
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
@@ -157,6 +187,10 @@ int Engine::init() {
     if ((rc = check(hipStreamCreateWithFlags(&copy_out_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
     if ((rc = check(hipEventCreateWithFlags(&ev_rs_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     if ((rc = check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate"))) return rc;
+    if ((rc = check(hipStreamCreateWithFlags(&copy_in_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
+        for (uint32_t i = 0; i < kPipeSlots; i++)
+            if ((rc = check(hipEventCreateWithFlags(&e[i], hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority).
     if (const char* env = getenv("CDA_RS_PRIORITY")) {
@@ -168,6 +202,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_HASH_SPLIT")) hash_split_ = atoi(env);
     if (const char* env = getenv("CDA_HOST_CHUNK")) host_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_HOST_PIPE_CHUNK")) host_pipe_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
@@ -248,6 +283,8 @@ uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n) const {
 }
 
 void Engine::order_begin(hipStream_t s) {
+    tl_in_call = true;
+    tl_call_stream = s;
     if (!order_used_) return;
     // the previous calls' work is complete (without a fault): nothing of it can
     // surface later, and there is nothing to order after (no wait packet ahead
@@ -260,6 +297,7 @@ void Engine::order_begin(hipStream_t s) {
 }
 
 void Engine::order_end(hipStream_t s) {
+    tl_in_call = false;
     if (order_ev_ && hipEventRecord(order_ev_, s) == hipSuccess) order_used_ = true;
 }
 
@@ -353,7 +391,9 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
         // 8- instead of 16-leaf subtrees; profiles/r03at/)
         const uint64_t want = subtree_lanes_ ? subtree_lanes_ : n_in >= 1024 ? 262144u : 131072u;
         while (sub < n_in && per_node * sub < want) sub *= 2;
-        bool fits = per_node * sub >= want && sub < n_in && n_in / sub >= (uint32_t)subtree_min_;
+        // launch_subtrees needs subtrees of >= 4 leaves: a smaller CDA_SUBTREE
+        // setting means per-level launches, not a failing launch
+        bool fits = per_node * sub >= want && sub < n_in && n_in / sub >= (uint32_t)std::max(subtree_min_, 4);
         const uint32_t slog = fits ? (uint32_t)__builtin_ctz(n_in / sub) : 0;
         for (uint32_t i = 0; i < n_forest && fits; i++) {
             const uint64_t need = (uint64_t)f[i].n_trees * sub * slog * kSlot;
@@ -868,14 +908,15 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
     for (auto& x : th) x.join();
 }
 
-int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds) {
+int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
+                               hipEvent_t ready, hipEvent_t done) {
     const size_t W = 2 * (size_t)k, sq_b = W * W * kShare, half = k * W * kShare;
     int rc;
-    if ((rc = check(hipEventRecord(ev_rs_, stream_), "hipEventRecord"))) return rc;
-    if ((rc = check(hipStreamWaitEvent(copy_out_, ev_rs_, 0), "hipStreamWaitEvent"))) return rc;
+    if ((rc = check(hipEventRecord(ready, from), "hipEventRecord"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(copy_out_, ready, 0), "hipStreamWaitEvent"))) return rc;
     if (host_full_d2h_) {   // the whole EDS back as one contiguous copy (Q0 included)
         if ((rc = check(hipMemcpyAsync(eds, d_eds, n * sq_b, hipMemcpyDeviceToHost, copy_out_), "D2H EDS"))) return rc;
-        return check(hipEventRecord(ev_out_, copy_out_), "hipEventRecord");
+        return check(hipEventRecord(done, copy_out_), "hipEventRecord");
     }
     for (uint32_t sq = 0; sq < n; sq++) {
         // Q1: rows 0..k-1, columns k..2k-1 (strided); Q2|Q3: the bottom half
@@ -888,7 +929,70 @@ int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uin
                         "D2H Q2|Q3")))
             return rc;
     }
-    return check(hipEventRecord(ev_out_, copy_out_), "hipEventRecord");
+    return check(hipEventRecord(done, copy_out_), "hipEventRecord");
+}
+
+// Big batches from host buffers (config 4 through the C ABI as a Go caller
+// would drive it: pkg/da/data_availability_header.go:65-75 takes host shares,
+// returns a host EDS).  Chunk i (slot i % kPipeSlots):
+//   copy_in_ : wait until chunk i - slots finished computing (its ODS slot is
+//              free), H2D of the chunk's ODS                        -> pipe_in_
+//   stream_  : wait for the H2D, and for chunk i - slots's parity to have left
+//              the EDS slot; RS                                      -> pipe_rs_
+//   copy_out_: wait for the RS, D2H of the three parity quadrants     -> pipe_d2h_
+//   stream_  : leaves, levels, roots and data roots of the chunk    -> pipe_comp_
+// so the H2D of chunk i+1, the compute of chunk i and the D2H of chunk i-1
+// run at once (PCIe is full duplex); the host copies Q0 (= the caller's ODS)
+// on its own threads meanwhile.
+int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
+                          uint8_t* roots, int32_t* status, uint32_t c) {
+    const uint32_t W = 2 * k;
+    const size_t ods_sq = (size_t)k * k * kShare, eds_sq = (size_t)W * W * kShare, root_sq = (size_t)W * kNode;
+    int rc;
+    if ((rc = check(h_ods_.ensure(kPipeSlots * c * ods_sq), "hipMalloc"))) return rc;
+    if ((rc = check(h_eds_.ensure(kPipeSlots * c * eds_sq), "hipMalloc"))) return rc;
+    if ((rc = check(h_rows_.ensure(n * root_sq), "hipMalloc"))) return rc;
+    if ((rc = check(h_cols_.ensure(n * root_sq), "hipMalloc"))) return rc;
+    if ((rc = check(h_roots_.ensure((size_t)n * 32), "hipMalloc"))) return rc;
+    if ((rc = check(err_buf_.ensure((size_t)n * 4), "hipMalloc"))) return rc;
+    hipStream_t s = stream_;
+    // the buffers' allocation (stream-ordered on s) precedes the copies
+    if ((rc = check(hipEventRecord(pipe_comp_[0], s), "hipEventRecord"))) return rc;
+    if ((rc = check(hipStreamWaitEvent(copy_in_, pipe_comp_[0], 0), "hipStreamWaitEvent"))) return rc;
+    HostPin pin_ods(host_register_, ods, (size_t)n * ods_sq, copy_in_, s),
+        pin_eds(host_register_, eds, (size_t)n * eds_sq, s, copy_out_);
+    uint32_t* err = err_buf_.as<uint32_t>();
+    for (uint32_t i = 0, i0 = 0; i0 < n; i++, i0 += c) {
+        const uint32_t m = std::min(c, n - i0), slot = i % kPipeSlots;
+        uint8_t* d_ods = h_ods_.as<uint8_t>() + slot * c * ods_sq;
+        uint8_t* d_eds = h_eds_.as<uint8_t>() + slot * c * eds_sq;
+        if (i >= kPipeSlots && (rc = check(hipStreamWaitEvent(copy_in_, pipe_comp_[slot], 0), "hipStreamWaitEvent")))
+            return rc;
+        if ((rc = check(hipMemcpyAsync(d_ods, ods + i0 * ods_sq, m * ods_sq, hipMemcpyHostToDevice, copy_in_), "H2D")))
+            return rc;
+        if ((rc = check(hipEventRecord(pipe_in_[slot], copy_in_), "hipEventRecord"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(s, pipe_in_[slot], 0), "hipStreamWaitEvent"))) return rc;
+        if (eds && i >= kPipeSlots && (rc = check(hipStreamWaitEvent(s, pipe_d2h_[slot], 0), "hipStreamWaitEvent")))
+            return rc;
+        if ((rc = enqueue_extend(d_ods, k, m, d_eds, s, err + i0))) return rc;
+        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * eds_sq, s, pipe_rs_[slot], pipe_d2h_[slot])))
+            return rc;
+        if ((rc = enqueue_dah(d_eds, k, m, h_rows_.as<uint8_t>() + i0 * root_sq, h_cols_.as<uint8_t>() + i0 * root_sq,
+                              h_roots_.as<uint8_t>() + (size_t)i0 * 32, err + i0, nullptr, s, true)))
+            return rc;
+        if ((rc = check(hipEventRecord(pipe_comp_[slot], s), "hipEventRecord"))) return rc;
+    }
+    if ((rc = check(hipMemcpyAsync(rows, h_rows_.ptr, n * root_sq, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(cols, h_cols_.ptr, n * root_sq, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if ((rc = check(hipMemcpyAsync(roots, h_roots_.ptr, (size_t)n * 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    std::vector<uint32_t> words(n);
+    if ((rc = check(hipMemcpyAsync(words.data(), err, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
+    if (eds && !host_full_d2h_) copy_q0(ods, k, n, eds);   // host work while the GPU runs
+    if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
+    if (eds && (rc = check(hipStreamSynchronize(copy_out_), "hipStreamSynchronize"))) return rc;
+    if (status)
+        for (uint32_t i = 0; i < n; i++) status[i] = words[i] == 0xFFFFFFFFu ? CDA_OK : CDA_ERR_PUSH_ORDER;
+    return push_order_error(words.data(), n, ods, k, false);
 }
 
 int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
@@ -896,6 +1000,11 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     const uint32_t W = 2 * k;
     const size_t ods_b = (size_t)n * k * k * kShare, eds_b = (size_t)n * W * W * kShare;
     const size_t roots_b = (size_t)n * W * kNode;
+    {   // big batches: the chunk pipeline (chunk ~ 256 MiB of ODS: 32 squares at k = 128)
+        const size_t ods_sq = (size_t)k * k * kShare;
+        const uint32_t c = host_pipe_chunk_ ? host_pipe_chunk_ : (uint32_t)std::max<size_t>(1, (256u << 20) / ods_sq);
+        if (n > 2 * c) return host_pipeline(ods, k, n, eds, rows, cols, roots, status, c);
+    }
     int rc;
     if ((rc = check(h_ods_.ensure(ods_b), "hipMalloc"))) return rc;
     if ((rc = check(h_eds_.ensure(eds_b), "hipMalloc"))) return rc;
@@ -921,7 +1030,9 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
         if ((rc = enqueue_extend(h_ods_.as<uint8_t>() + i0 * ods_sq, k, m, h_eds_.as<uint8_t>() + i0 * eds_sq, s,
                                  err_buf_.as<uint32_t>() + i0)))
             return rc;
-        if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>() + i0 * eds_sq, k, m, eds + i0 * eds_sq))) return rc;
+        if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>() + i0 * eds_sq, k, m, eds + i0 * eds_sq, s, ev_rs_,
+                                            ev_out_)))
+            return rc;
     }
     if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, n, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
                           h_roots_.as<uint8_t>(), err_buf_.as<uint32_t>(), nullptr, s, true)))
@@ -951,7 +1062,7 @@ int Engine::host_extend(const uint8_t* ods, uint32_t k, uint8_t* eds) {
         pin_eds(host_register_, eds, eds_b, stream_, copy_out_);
     if ((rc = check(hipMemcpyAsync(h_ods_.ptr, ods, ods_b, hipMemcpyHostToDevice, s), "H2D"))) return rc;
     if ((rc = enqueue_extend(h_ods_.as<uint8_t>(), k, 1, h_eds_.as<uint8_t>(), s))) return rc;
-    if ((rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, 1, eds))) return rc;
+    if ((rc = enqueue_parity_d2h(h_eds_.as<uint8_t>(), k, 1, eds, s, ev_rs_, ev_out_))) return rc;
     copy_q0(ods, k, 1, eds);
     return check(hipEventSynchronize(ev_out_), "hipEventSynchronize");
 }

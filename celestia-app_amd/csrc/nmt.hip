@@ -40,9 +40,6 @@ constexpr size_t SH = 512;
 #ifndef CDA_LEVEL_WAVES
 #define CDA_LEVEL_WAVES 4
 #endif
-#ifndef CDA_LEAF_PREFETCH
-#define CDA_LEAF_PREFETCH 1
-#endif
 
 __device__ __forceinline__ void load_chunk(const uint4* p, uint32_t (&w)[16]) {
 #pragma unroll
@@ -124,10 +121,8 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
     sha_init(st);
     uint32_t cur[16], tail[8], w[16];
     load_raw16(src, cur);
-#if CDA_LEAF_PREFETCH
-    uint32_t nxt[16];
+    uint32_t nxt[16];   // the next 64-B chunk in flight during each block
     load_raw16(src + 4, nxt);
-#endif
     // block 0: 0x00 || ns(29) || share[0:34]; a parity leaf's first 7 words
     // are constant, so it starts from the precomputed mid-state
 #pragma unroll
@@ -147,13 +142,9 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
 
 #pragma unroll 1
     for (int b = 1; b < 8; b++) {
-#if CDA_LEAF_PREFETCH
 #pragma unroll
         for (int i = 0; i < 16; i++) cur[i] = nxt[i];
         if (b < 7) load_raw16(src + 4 * (b + 1), nxt);
-#else
-        load_raw16(src + 4 * b, cur);
-#endif
 #pragma unroll
         for (int t = 0; t < 7; t++) w[t] = body_word(tail[t], tail[t + 1]);
         w[7] = body_word(tail[7], cur[0]);
@@ -323,16 +314,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
 // operands (a leaf pair, or a stored left sibling) at use: 141 VGPRs, three
 // waves per SIMD, whose loads hide behind each other's hashing -- against
 // round 3's first form, which loaded them one iteration ahead as raw words
-// (189 VGPRs, two waves per SIMD; CDA_SUBTREE_NOPF=0 builds it): config 4's
+// (189 VGPRs, two waves per SIMD; tools/probes/subtree_prefetch.patch): config 4's
 // levels 14.06 -> 13.90 ms, one k = 512 square unchanged (profiles/r03ar/).
 // Pending left siblings go to a per-lane stack in the forest's output buffer
 // behind the subtree roots (written and read by the same lane).  A wave is
 // 64 consecutive trees of one subtree index, so the parity mid-state branch
 // of hash_node stays uniform.
 // ---------------------------------------------------------------------------
-#ifndef CDA_SUBTREE_NOPF
-#define CDA_SUBTREE_NOPF 1
-#endif
 __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx,
                                                       uint32_t nsq, uint32_t nblocks) {
     const uint32_t S = 1u << slog;
@@ -353,10 +341,6 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
         auto stack_slot = [&](uint32_t l) -> uint8_t* {
             return out + ((size_t)lanes + (size_t)(l - 1) * lanes + idx) * kSlot;
         };
-        // next operands as RAW little-endian words: byte-swapped only when
-        // they are used, one iteration later (a swap right after the load
-        // would make the compiler wait for it there)
-        uint4 nL[6], nR[6];
         uint32_t cur[kSlotWords];
         auto load_raw = [](const uint8_t* p, uint4 (&q)[6]) {
             const uint4* v = reinterpret_cast<const uint4*>(p);
@@ -370,9 +354,7 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
                 w[4 * i + 2] = bswap32(q[i].z); w[4 * i + 3] = bswap32(q[i].w);
             }
         };
-#if CDA_SUBTREE_NOPF
-        (void)nL; (void)nR;
-        uint32_t j = 0, lvl = 0, pos = 0;
+        uint32_t j = 0, lvl = 0, pos = 0;   // next leaf pair; level / index of cur
 #pragma unroll 1
         for (uint32_t it = 0; it + 1 < S; it++) {
             const bool merge = it > 0 && (pos & 1);
@@ -395,42 +377,6 @@ __global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t
             lvl = nlvl;
             pos = npos;
         }
-#else
-        load_raw(in, nL);
-        load_raw(in + leaf_step, nR);
-        uint32_t j = 0;               // next unconsumed leaf pair (pair 0 is in nL / nR)
-        uint32_t lvl = 0, pos = 0;    // level / index of cur
-#pragma unroll 1
-        for (uint32_t it = 0; it + 1 < S; it++) {
-            // cur is a right child: hash it with its stored left sibling;
-            // otherwise the next leaf pair
-            const bool merge = it > 0 && (pos & 1);
-            uint32_t L[kSlotWords], R[kSlotWords];
-            be(nL, L);
-            if (merge) {
-#pragma unroll
-                for (int i = 0; i < kSlotWords; i++) R[i] = bswap32(cur[i]);
-            } else {
-                be(nR, R);
-            }
-            const uint32_t nlvl = merge ? lvl + 1 : 1u, npos = merge ? pos >> 1 : j;
-            if (!merge) j++;
-            // the next iteration's memory operands, in flight during this
-            // hash: always both loads, from branch-free addresses (the stored
-            // left sibling twice before a merge; this subtree's first leaves
-            // after the last iteration), so no control-flow join forces an
-            // early wait on them
-            const bool more = it + 2 < S, sib = (npos & 1) != 0;
-            const uint8_t* pa = !more ? in : sib ? stack_slot(nlvl) : in + (size_t)(2 * j) * leaf_step;
-            const uint8_t* pb = !more ? in : sib ? pa : in + (size_t)(2 * j + 1) * leaf_step;
-            load_raw(pa, nL);
-            load_raw(pb, nR);
-            hash_node(L, R, cur);
-            if (!(npos & 1) && nlvl < slog) store_slot(stack_slot(nlvl), cur);
-            lvl = nlvl;
-            pos = npos;
-        }
-#endif
         if (top == 1) {   // whole trees: the roots, as level_kernel's last level writes them
             if (F.roots) {
                 uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);

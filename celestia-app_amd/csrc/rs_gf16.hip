@@ -1014,6 +1014,12 @@ hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s)
 hipError_t launch_rs(const RsJob& j, uint32_t k, uint32_t n, const Gf16Dev& t, hipStream_t s) {
     if (k == 0 || (k & (k - 1))) return hipErrorInvalidValue;
     if (k <= 128) return launch_rs8_job(j, k, n, s);
+    // bitsliced encoder (rs_gf16_bs.hip); CDA_RS16_BS=0 runs the v_perm form (A/B)
+    static const bool bs = [] {
+        const char* e = getenv("CDA_RS16_BS");
+        return e ? atoi(e) != 0 : true;
+    }();
+    if (bs && (k == 256 || k == 512)) return launch_rs16_bs(j, k, n, s);
     if (t.chunk && t.chunk_k == k) {
         if (k == 256) return launch_cw<256>(t, j, n, s);
         if (k == 512) return launch_cw<512>(t, j, n, s);

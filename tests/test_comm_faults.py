@@ -153,3 +153,53 @@ def test_comm_abort_without_lock(ctx, comm_setup):
     c.comm_init(0, 1, _lib.comm_unique_id())
     _clean_split_matches(ctx, c, d_ods, k)
 
+
+
+def test_peer_failure_fails_rank0(ctx, comm_setup):
+    """a peer's local failure reaches rank 0 only as a 0 in the
+    MIN-reduced push-order word; rank 0 must then return an error (not CDA_OK
+    with roots combined from whatever arrived).  CDA_COMM_FAULT=peer poisons
+    the word before the reduce as a failed peer would."""
+    from celestia_da import _lib
+    c, d_ods, k = comm_setup
+    os.environ["CDA_COMM_FAULT"] = "peer"
+    rc, msg, word = _split_rc(c, d_ods, k)
+    assert rc == _lib.CDA_ERR_DEVICE and "peer rank failed" in msg, (rc, msg)
+    assert word == 0
+    os.environ.pop("CDA_COMM_FAULT")
+    _clean_split_matches(ctx, c, d_ods, k)
+
+
+def test_abort_from_watchdog_during_agreement(ctx, comm_setup):
+    """cda_comm_abort from another thread while the call waits in
+    the agreement round (CDA_COMM_FAULT=stall holds it there as if a peer never
+    arrived) must release the call with CDA_ERR_COMM, without touching the
+    aborted communicator afterwards; a fresh communicator then works."""
+    import threading
+    import time
+
+    import torch
+    from celestia_da import _lib, testfactory
+    c, d_ods, k = comm_setup
+    _clean_split_matches(ctx, c, d_ods, k)
+    k2 = 32   # a new k: the agreement round runs again
+    d2 = torch.from_numpy(testfactory.random_square(k2, 11)).to(d_ods.device)
+    os.environ["CDA_COMM_FAULT"] = "stall"
+    out = {}
+
+    def call():
+        out["r"] = _split_rc(c, d2, k2)
+
+    t = threading.Thread(target=call)
+    t0 = time.monotonic()
+    t.start()
+    time.sleep(0.5)
+    c.comm_abort()
+    t.join(timeout=60)
+    assert not t.is_alive()
+    rc, msg, _ = out["r"]
+    assert rc == _lib.CDA_ERR_COMM and "aborted during the call" in msg, (rc, msg)
+    assert time.monotonic() - t0 < 20
+    os.environ.pop("CDA_COMM_FAULT")
+    c.comm_init(0, 1, _lib.comm_unique_id())
+    _clean_split_matches(ctx, c, d2, k2)
