@@ -234,9 +234,11 @@ def host_pipeline_rates(ctx, k: int, d_ods, d_eds, idx, reps: int = 3) -> dict:
     status = np.zeros(n, dtype=np.int32)
     st = status.ctypes.data_as(C.POINTER(C.c_int32))
 
+    def tptr(t):   # a pinned tensor as the uint8_t* the C ABI takes
+        return C.cast(C.c_void_p(t.data_ptr()), C.POINTER(C.c_ubyte))
+
     def run(with_eds):
-        ctx.check(ctx.lib.cda_extend_dah_batch(ctx.h, C.c_void_p(h_ods.data_ptr()), k, n,
-                                               C.c_void_p(h_eds.data_ptr()) if with_eds else None,
+        ctx.check(ctx.lib.cda_extend_dah_batch(ctx.h, tptr(h_ods), k, n, tptr(h_eds) if with_eds else None,
                                                ptr(rows), ptr(cols), ptr(roots), st))
 
     def med(f):

@@ -207,10 +207,10 @@ B16_HD uint32_t bitsel(uint32_t a, uint32_t b, uint32_t m) {
 #endif
 }
 
-// acc XOR the planes y[j] for the set bits j of MSK, as 3-input XORs.
+// acc XOR the signals y[j] for the set bits j of MSK, as 3-input XORs.
 template <uint32_t MSK, int J = 0>
 B16_HD uint32_t xor_fold(uint32_t acc, const uint32_t* y) {
-    if constexpr (J >= 16 || (MSK >> J) == 0) {
+    if constexpr (J >= 32 || (MSK >> J) == 0) {
         return acc;
     } else if constexpr (((MSK >> J) & 1) == 0) {
         return xor_fold<MSK, J + 1>(acc, y);
@@ -251,15 +251,51 @@ B16_HD uint32_t xor_and(uint32_t x, uint32_t p, uint32_t m) {
     return x ^ (p & m);
 #endif
 }
-// x ^= (c*y) & m for a per-lane all-ones / all-zero mask m: the product by one
-// basis term of a lane-dependent constant.
+
+// Pair signals: a butterfly's networks all read the same 16 planes y, so the
+// 8 pair sums y[2i] ^ y[2i+1] are formed once (S[16 + i]) and a row picks, per
+// pair, y[2i], y[2i+1] or their sum: about 3/4 of the terms of the plain row
+// (the LOW phase's networks: -20 % instructions for 8 registers).
+struct Sig24 {
+    uint32_t s[24];
+};
+B16_HD void make_sig(Sig24& S, const uint32_t* y) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) S.s[j] = y[j];
+#pragma unroll
+    for (int i = 0; i < 8; i++) S.s[16 + i] = y[2 * i] ^ y[2 * i + 1];
+}
+// a row over 16 planes -> the same sum over the 24 signals
+constexpr uint32_t pair_terms(uint32_t row) {
+    uint32_t t = 0;
+    for (int i = 0; i < 8; i++) {
+        const uint32_t c = (row >> (2 * i)) & 3;
+        if (c == 1) t |= 1u << (2 * i);
+        if (c == 2) t |= 1u << (2 * i + 1);
+        if (c == 3) t |= 1u << (16 + i);
+    }
+    return t;
+}
+// x ^= c*y from the signals of y
 template <uint32_t C>
-B16_HD void mul_add_masked(uint32_t* x, const uint32_t* y, uint32_t m) {
+B16_HD void mul_add_s(uint32_t* x, const Sig24& S) {
     if constexpr (C != 0) {
         constexpr Net n = make_net(C);
         sfor<0, 16, 1>([&](auto ii) {
             constexpr int i = decltype(ii)::value;
-            if constexpr (n.row[i] != 0) x[i] = xor_and(x[i], xor_sel<n.row[i]>(y), m);
+            x[i] = xor_fold<pair_terms(n.row[i])>(x[i], S.s);
+        });
+    }
+}
+// x ^= (c*y) & m for a per-lane all-ones / all-zero mask m: the product by one
+// basis term of a lane-dependent constant.
+template <uint32_t C>
+B16_HD void mul_add_masked_s(uint32_t* x, const Sig24& S, uint32_t m) {
+    if constexpr (C != 0) {
+        constexpr Net n = make_net(C);
+        sfor<0, 16, 1>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            if constexpr (n.row[i] != 0) x[i] = xor_and(x[i], xor_sel<pair_terms(n.row[i])>(S.s), m);
         });
     }
 }
@@ -346,32 +382,40 @@ B16_HD void xor_pairs(uint32_t* R) {   // y ^= x for the pairs (i, i + D) of 8 u
 }
 // One layer over the 8 units: unit distance D, shard bit b, the unit index
 // holding shard bits from SH up (group bits of unit i: (i & ~(2D-1)) << SH),
-// NL masked lane terms (shard bits LB..), NW_ uniform wave terms (bits WB..).
+// NL masked lane terms (shard bits LB..), NWB uniform wave terms (bits WB..).
+// Per butterfly the pair signals of y are formed once and every term reads
+// them; the wave terms are uniform branches.
 template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB>
 B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
-    if constexpr (INV) xor_pairs<D>(R);
     sfor<0, 8, 1>([&](auto ii) {
         constexpr int i = decltype(ii)::value;
         if constexpr ((i & D) == 0) {
+            uint32_t* x = R + 16 * i;
+            uint32_t* y = R + 16 * (i + D);
+            if constexpr (INV) {
+#pragma unroll
+                for (int p = 0; p < 16; p++) y[p] ^= x[p];
+            }
+            Sig24 S;
+            make_sig(S, y);
             constexpr uint32_t C0 = skew_part<INV, LOGK>(b, (uint32_t)(i & ~(2 * D - 1)) << SH);
-            mul_add<C0>(R + 16 * i, R + 16 * (i + D));
+            mul_add_s<C0>(x, S);
             sfor<0, NL, 1>([&](auto ll) {
                 constexpr int l = decltype(ll)::value;
-                mul_add_masked<tbasis(b, LB + l)>(R + 16 * i, R + 16 * (i + D), m[l]);
+                mul_add_masked_s<tbasis(b, LB + l)>(x, S, m[l]);
             });
+            sfor<0, NWB, 1>([&](auto ww) {
+                constexpr int w = decltype(ww)::value;
+                if (u & (1u << w)) mul_add_s<tbasis(b, WB + w)>(x, S);
+            });
+            if constexpr (!INV) {
+#pragma unroll
+                for (int p = 0; p < 16; p++) y[p] ^= x[p];
+            }
+            fence<16>(x);
+            fence<16>(y);
         }
     });
-    sfor<0, NWB, 1>([&](auto ww) {
-        constexpr int w = decltype(ww)::value;
-        if (u & (1u << w)) {
-            sfor<0, 8, 1>([&](auto ii) {
-                constexpr int i = decltype(ii)::value;
-                if constexpr ((i & D) == 0) mul_add<tbasis(b, WB + w)>(R + 16 * i, R + 16 * (i + D));
-            });
-        }
-    });
-    if constexpr (!INV) xor_pairs<D>(R);
-    fence<128>(R);
 }
 // LOW layer b (0..2): unit = shard bits 0..2, lane bits 3..6 (m[0..3]), wave bits 7..
 template <int LOGK, bool INV, int b>

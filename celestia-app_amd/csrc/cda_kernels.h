@@ -44,19 +44,7 @@ struct Gf16Dev {
     const uint16_t* log;   // 65536
     const uint16_t* exp;   // 65536
     const uint16_t* skew;  // 65535
-    // Per-k multiply tables for the register-resident encoder (k = 256, 512):
-    // chunk[idx][16] = 2-bit-chunk v_perm tables of the constant skew[idx]
-    // (all zero when skew[idx] is the modulus, i.e. "multiply by zero").
-    const uint32_t* chunk = nullptr;
-    uint32_t chunk_k = 0;
 };
-// Dwords per constant in `chunk` (rs_gf16.hip mul_add16): 3-bit chunks by
-// default (24), the 2-bit-chunk layout (16) with -DCDA_RS16_CHUNK2.
-#ifdef CDA_RS16_CHUNK2
-constexpr uint32_t kGf16TabWords = 16;
-#else
-constexpr uint32_t kGf16TabWords = 24;
-#endif
 
 // Leopard encode of every codeword of `job` for n_squares squares; k data
 // shards of 512 B per codeword (GF(2^8) for k <= 128, GF(2^16) above).

@@ -326,7 +326,6 @@ class Engine {
     std::mutex mu_;
     std::string err_;
     DevBuf gf16_log_, gf16_exp_, gf16_skew_;
-    DevBuf gf16_chunk_[2];   // k = 256, 512
     Gf16Dev gf16(uint32_t k) const;
     DevBuf leaf_, lvl_, root_slots_, dig_, err_buf_, dev_err_;
     DevBuf h_ods_, h_eds_, h_rows_, h_cols_, h_roots_;   // device staging for host-buffer calls

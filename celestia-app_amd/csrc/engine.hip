@@ -79,7 +79,7 @@ Engine::Engine(int device) : device_(device) {}
 
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
-    for (DevBuf* b : {&gf16_chunk_[0], &gf16_chunk_[1], &gf16_log_, &gf16_exp_,
+    for (DevBuf* b : {&gf16_log_, &gf16_exp_,
                       &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &dev_err_, &h_ods_, &h_eds_,
                       &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_, &cm_plan_, &cm_tables_,
                       &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_, &gf8_log_, &gf8_exp_, &gf8_skew_, &rp_cw_,
@@ -220,53 +220,12 @@ int Engine::init() {
     if ((rc = check(hipMemcpy(gf16_exp_.ptr, F->exp, sizeof F->exp, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     if ((rc = check(hipMemcpy(gf16_skew_.ptr, F->skew, sizeof F->skew, hipMemcpyHostToDevice), "hipMemcpy")))
         return rc;
-    // 2-bit-chunk v_perm tables for the constants of the k = 256 / 512 schedules
-    for (int v = 0; v < 2; v++) {
-        const uint32_t k = v == 0 ? 256 : 512, n = 2 * k - 1;
-        std::vector<uint32_t> tab((size_t)n * kGf16TabWords, 0);
-        for (uint32_t idx = 0; idx < n; idx++) {
-            const uint32_t L = F->skew[idx];
-            if (L == LeoField<16>::MOD) continue;    // multiply by zero: all-zero tables
-            uint32_t* t = tab.data() + (size_t)idx * kGf16TabWords;
-            // put entry e (product of e << shift) into byte `slot` of dword pair
-            // (lo output byte, hi output byte) at t[w], t[w + 1]
-            auto put = [&](uint32_t w, uint32_t e, uint32_t shift, uint32_t slot) {
-                const uint32_t prod = F->mul_log(e << shift, L);
-                t[w] |= (prod & 0xFFu) << (8 * slot);
-                t[w + 1] |= (prod >> 8) << (8 * slot);
-            };
-#ifdef CDA_RS16_CHUNK2
-            for (uint32_t q = 0; q < 8; q++)   // 2-bit chunk q of the symbol, entries 0..3
-                for (uint32_t e = 0; e < 4; e++) put(2 * q, e, q < 4 ? 2 * q : 8 + 2 * (q - 4), e);
-#else
-            // 3-bit chunks a = 0..3 at bits 0, 3 (lo byte) and 8, 11 (hi byte):
-            // entries 4..7 in t[2a], t[2a+1] (v_perm src0, SGPR), entries
-            // 0..3 in t[12+2a], t[13+2a] (src1, copied to VGPRs); 2-bit chunks at
-            // bits 6 and 14: entries 0..3 in t[8..9] and t[10..11]
-            const uint32_t sh3[4] = {0, 3, 8, 11};
-            for (uint32_t a = 0; a < 4; a++)
-                for (uint32_t e = 0; e < 8; e++) put(e < 4 ? 12 + 2 * a : 2 * a, e, sh3[a], e & 3);
-            for (uint32_t e = 0; e < 4; e++) {
-                put(8, e, 6, e);
-                put(10, e, 14, e);
-            }
-#endif
-        }
-        if ((rc = check(gf16_chunk_[v].ensure(tab.size() * 4), "hipMalloc"))) return rc;
-        if ((rc = check(hipMemcpy(gf16_chunk_[v].ptr, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "hipMemcpy")))
-            return rc;
-    }
     return CDA_OK;
 }
 
 Gf16Dev Engine::gf16(uint32_t k) const {
-    Gf16Dev t{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
-    if (k == 256 || k == 512) {
-        const int v = k == 256 ? 0 : 1;
-        t.chunk = gf16_chunk_[v].as<uint32_t>();
-        t.chunk_k = k;
-    }
-    return t;
+    (void)k;   // k = 256 / 512 use compile-time networks (rs_gf16_bs.hip); the tables serve other k
+    return Gf16Dev{gf16_log_.as<uint16_t>(), gf16_exp_.as<uint16_t>(), gf16_skew_.as<uint16_t>()};
 }
 
 static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }

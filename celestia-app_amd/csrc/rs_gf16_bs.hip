@@ -35,16 +35,16 @@ namespace cda {
 
 namespace {
 
+// Three workgroups per CU (168 VGPRs, 32 KiB of LDS each): a CU always has
+// a third wave on each SIMD to issue while one waits at a barrier or on
+// memory; at two per CU (208 VGPRs, no spills) the encoder was 15-20 % slower
+// (profiles/r04d/, r04f/).  Prefetching the next round's codewords into L2 /
+// MALL with LDS-DMA during the compute phases was slower still (r04d).
+constexpr int kWavesPerSimd = 3;
 // Exchange buffer: kChunksPerRound 16-byte chunks (4 planes) of every unit of
-// the workgroup per round; 8 consecutive lanes always address 8 distinct
-// 16-byte bank groups (see the slot functions).
-#ifndef CDA_BS16_CHUNKS   // tuning A/B (r04): chunks per exchange round
-#define CDA_BS16_CHUNKS 2
-#endif
-#ifndef CDA_BS16_WPE      // tuning A/B (r04): waves per SIMD the kernel is register-sized for
-#define CDA_BS16_WPE 2
-#endif
-constexpr int kChunksPerRound = CDA_BS16_CHUNKS;
+// the workgroup per round (four rounds per exchange); 8 consecutive lanes
+// always address 8 distinct 16-byte bank groups (see the slot functions).
+constexpr int kChunksPerRound = 1;
 template <int LOGK>
 constexpr uint32_t bs16_lds_bytes() {
     return (uint32_t)kChunksPerRound * (1u << LOGK) * 4 * 16;   // shards x 4 blocks x 16 B per chunk
@@ -64,7 +64,7 @@ __device__ __forceinline__ void lds_ld(const u32x4* X, uint32_t idx, uint32_t* r
 }
 
 template <int LOGK>
-__global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_eu(CDA_BS16_WPE))) void rs16_bs_kernel(
+__global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd))) void rs16_bs_kernel(
     const RsJob job) {
     constexpr int NW = 1 << (LOGK - 7);    // waves per workgroup
     constexpr int K = 1 << LOGK;

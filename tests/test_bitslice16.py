@@ -13,7 +13,8 @@
 * test_kernel_is_full_rate: the gfx950 ISA of rs16_bs_kernel holds no
   half-rate VALU op beyond a few prologue address computations (v_perm, v_alignbit, 64-bit shifts, 3-operand adds/ors,
   bfi -- DESIGN.md 3.1: one in the stream makes every instruction issue at
-  4 cycles) and no scratch, within 256 VGPRs (two waves per SIMD).
+  4 cycles), within 168 VGPRs (three waves per SIMD) and with at most a
+  few dozen spilled values.
 """
 import os
 import re
@@ -62,4 +63,8 @@ def test_kernel_is_full_rate():
         meta = s[s.index(".Lfunc_end", pos):]
         vg = int(re.search(r"NumVgprs: (\d+)", meta).group(1))
         scratch = int(re.search(r"ScratchSize: (\d+)", meta).group(1))
-        assert vg <= 256 and scratch == 0, (name, vg, scratch)
+        # three waves per SIMD (168 VGPRs); the few dozen long-lived values the
+        # register cap spills (addresses, lane masks) are reloaded once per
+        # phase, not inside the networks
+        n_scratch = len(re.findall(r"^\s+scratch_(?:load|store)", body, re.M))
+        assert vg <= 168 and scratch <= 256 and n_scratch <= 0.02 * len(ops), (name, vg, scratch, n_scratch)

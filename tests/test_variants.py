@@ -2,8 +2,9 @@
 
 The library picks one kernel per job shape and reads its A/B knobs once per
 process, so the non-default forms are only reachable from a fresh process:
-  * CDA_RS16_HALF=0 -- the full-width GF(2^16) codeword kernel (one 1024-thread
-    workgroup per codeword) instead of the default two half-width workgroups;
+  * (round 3's CDA_RS16_HALF=0 full-width GF(2^16) kernel was removed in round 4
+    with the byte-form encoders it belonged to; the bitsliced encoder has no
+    variants)
   * CDA_RS8_SLICE=0 -- the k = 128 Q0 launch of a batch without the XCD-aware
     128-byte slices (mode 0, two codewords per workgroup);
   * CDA_RS8_BS=1 -- round 1's four-codeword k = 128 encoder.
@@ -58,15 +59,6 @@ def _run(env_extra: dict, k: int, n: int) -> list:
                        text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
-
-
-def test_full_width_gf16_kernel_matches_fixture():
-    g = json.load(open(os.path.join(HERE, "golden", "k512.json")))["squares"]
-    got = _run({"CDA_RS16_HALF": "0"}, 512, 2)
-    for i in (0, 1):
-        assert got[i]["status"] == 0
-        assert got[i]["eds_sha256"] == g[str(i)]["eds_sha256"], i
-        assert got[i]["data_root"] == g[str(i)]["data_root"], i
 
 
 @pytest.mark.parametrize("env", [{"CDA_RS8_SLICE": "0"}, {"CDA_RS8_SLICE": "1"}, {"CDA_RS8_BS": "1"}],

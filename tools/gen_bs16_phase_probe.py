@@ -11,7 +11,7 @@ import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = open(os.path.join(ROOT, "celestia-app_amd", "csrc", "rs_gf16_bs.hip")).read()
-head = src[src.index("// Exchange buffer"):src.index("template <int LOGK>\n__global__")]
+head = src[src.index("// Three workgroups per CU"):src.index("template <int LOGK>\n__global__")]
 k0 = src.index("template <int LOGK>\n__global__")
 k1 = src.index("template <int LOGK>\nhipError_t launch_bs")
 kern = src[k0:k1]

@@ -3,12 +3,12 @@
 set -e
 mkdir -p gpurun_out/r04d
 cd $GRAFT_REPO_ROOT
-timeout -k 10 120 ./tools/bs16_phase_probe 4 > gpurun_out/r04d/phase.txt 2>&1 || true
 for rep in 1 2; do
-for v in prod bs3 bs2c1 vperm; do
+for v in bs3 bs3pf bs2pf vperm; do
   L=$PWD/celestia-app_amd/libcda.so; X=1
   [ $v = bs3 ] && L=$PWD/celestia-app_amd/build_var/bs3/libcda.so
-  [ $v = bs2c1 ] && L=$PWD/celestia-app_amd/build_var/bs2c1/libcda.so
+  [ $v = bs3pf ] && L=$PWD/celestia-app_amd/build_var/bs3pf/libcda.so
+  [ $v = bs2pf ] && L=$PWD/celestia-app_amd/build_var/bs2pf/libcda.so
   [ $v = vperm ] && X=0
   for b in 1 4; do
     CDA_LIB=$L CDA_RS16_BS=$X timeout -k 10 150 python bench.py --k 512 --batch $b --no-cpu --no-extras --steps 20 > gpurun_out/r04d/ab_${v}_$b.log 2>&1
