@@ -280,13 +280,15 @@ class Engine {
     hipStream_t copy_out_ = nullptr;
     hipEvent_t ev_rs_ = nullptr, ev_out_ = nullptr;
     int enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
-                           hipEvent_t ready, hipEvent_t done);
+                           hipEvent_t ready, hipEvent_t done, hipStream_t q1 = nullptr, hipEvent_t q1_done = nullptr);
     // Big host-buffer batches (host_extend_dah, n > 2 chunks): chunks of
     // squares through a ring of kPipeSlots device slots, H2D on copy_in_,
     // extension + hashing on stream_, parity D2H on copy_out_, so chunk i+1
     // goes up while chunk i computes and chunk i-1 comes down.
     static constexpr uint32_t kPipeSlots = 3;
-    hipStream_t copy_in_ = nullptr;
+    hipStream_t copy_in_ = nullptr, copy_q1_ = nullptr;
+    hipEvent_t pipe_q1_[kPipeSlots] = {};
+    bool host_d2h2_ = true;   // CDA_HOST_D2H2: the 2-D Q1 copies on their own stream (A/B)
     hipEvent_t pipe_in_[kPipeSlots] = {}, pipe_rs_[kPipeSlots] = {}, pipe_d2h_[kPipeSlots] = {},
                pipe_comp_[kPipeSlots] = {};
     uint32_t host_pipe_chunk_ = 0;   // CDA_HOST_PIPE_CHUNK: squares per chunk (0 = auto: ~256 MiB of ODS)

@@ -101,10 +101,11 @@ Engine::~Engine() {
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (ev_rs_) (void)hipEventDestroy(ev_rs_);
     if (ev_out_) (void)hipEventDestroy(ev_out_);
-    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
+    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_, pipe_q1_})
         for (uint32_t i = 0; i < kPipeSlots; i++)
             if (e[i]) (void)hipEventDestroy(e[i]);
     if (copy_in_) (void)hipStreamDestroy(copy_in_);
+    if (copy_q1_) (void)hipStreamDestroy(copy_q1_);
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
@@ -188,7 +189,9 @@ int Engine::init() {
     if ((rc = check(hipEventCreateWithFlags(&ev_rs_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     if ((rc = check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     if ((rc = check(hipStreamCreateWithFlags(&copy_in_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
-    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
+    if ((rc = check(hipStreamCreateWithFlags(&copy_q1_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    if (const char* env = getenv("CDA_HOST_D2H2")) host_d2h2_ = atoi(env) != 0;
+    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_, pipe_q1_})
         for (uint32_t i = 0; i < kPipeSlots; i++)
             if ((rc = check(hipEventCreateWithFlags(&e[i], hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
@@ -868,7 +871,7 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
 }
 
 int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
-                               hipEvent_t ready, hipEvent_t done) {
+                               hipEvent_t ready, hipEvent_t done, hipStream_t q1, hipEvent_t q1_done) {
     const size_t W = 2 * (size_t)k, sq_b = W * W * kShare, half = k * W * kShare;
     int rc;
     if ((rc = check(hipEventRecord(ready, from), "hipEventRecord"))) return rc;
@@ -877,16 +880,23 @@ int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uin
         if ((rc = check(hipMemcpyAsync(eds, d_eds, n * sq_b, hipMemcpyDeviceToHost, copy_out_), "D2H EDS"))) return rc;
         return check(hipEventRecord(done, copy_out_), "hipEventRecord");
     }
+    // Q1 (rows 0..k-1, columns k..2k-1: strided) as 2-D copies -- on stream q1
+    // when given, so they run beside the linear Q2|Q3 copies
+    hipStream_t sq1 = q1 ? q1 : copy_out_;
+    if (q1 && (rc = check(hipStreamWaitEvent(q1, ready, 0), "hipStreamWaitEvent"))) return rc;
     for (uint32_t sq = 0; sq < n; sq++) {
-        // Q1: rows 0..k-1, columns k..2k-1 (strided); Q2|Q3: the bottom half
         if ((rc = check(hipMemcpy2DAsync(eds + sq * sq_b + k * kShare, W * kShare, d_eds + sq * sq_b + k * kShare,
-                                         W * kShare, (size_t)k * kShare, k, hipMemcpyDeviceToHost, copy_out_),
+                                         W * kShare, (size_t)k * kShare, k, hipMemcpyDeviceToHost, sq1),
                         "D2H Q1")))
             return rc;
         if ((rc = check(hipMemcpyAsync(eds + sq * sq_b + half, d_eds + sq * sq_b + half, half, hipMemcpyDeviceToHost,
                                        copy_out_),
                         "D2H Q2|Q3")))
             return rc;
+    }
+    if (q1) {
+        if ((rc = check(hipEventRecord(q1_done, q1), "hipEventRecord"))) return rc;
+        if ((rc = check(hipStreamWaitEvent(copy_out_, q1_done, 0), "hipStreamWaitEvent"))) return rc;
     }
     return check(hipEventRecord(done, copy_out_), "hipEventRecord");
 }
@@ -934,7 +944,8 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
         if (eds && i >= kPipeSlots && (rc = check(hipStreamWaitEvent(s, pipe_d2h_[slot], 0), "hipStreamWaitEvent")))
             return rc;
         if ((rc = enqueue_extend(d_ods, k, m, d_eds, s, err + i0))) return rc;
-        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * eds_sq, s, pipe_rs_[slot], pipe_d2h_[slot])))
+        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * eds_sq, s, pipe_rs_[slot], pipe_d2h_[slot],
+                                            host_d2h2_ ? copy_q1_ : nullptr, pipe_q1_[slot])))
             return rc;
         if ((rc = enqueue_dah(d_eds, k, m, h_rows_.as<uint8_t>() + i0 * root_sq, h_cols_.as<uint8_t>() + i0 * root_sq,
                               h_roots_.as<uint8_t>() + (size_t)i0 * 32, err + i0, nullptr, s, true)))

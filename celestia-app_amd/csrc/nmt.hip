@@ -321,7 +321,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
 // 64 consecutive trees of one subtree index, so the parity mid-state branch
 // of hash_node stays uniform.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void subtree_kernel(const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx,
+#ifndef CDA_SUBTREE_WPE   // experiment (r04): waves per SIMD the subtree kernel is register-sized for
+#define CDA_SUBTREE_WPE 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_SUBTREE_WPE))) void subtree_kernel(const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx,
                                                       uint32_t nsq, uint32_t nblocks) {
     const uint32_t S = 1u << slog;
     const uint32_t top = n_in >> slog;   // subtree roots per tree

@@ -141,9 +141,11 @@ int cda_extend_dah_device(cda_ctx *ctx, const void *d_ods, uint32_t k, uint32_t 
                           void *d_col_roots, void *d_data_roots, int32_t *d_status, void *stream);
 
 /* Size the context's scratch for device batches of up to n squares of width
- * k (synchronous).  Scratch buffers only grow, and growing one drains the
- * device first (hipFree does); after cda_reserve the device entry points for
- * batches up to that size stay purely enqueue-only. */
+ * k (synchronous).  Scratch buffers only grow; inside a call a growing buffer
+ * is released and reallocated in stream order on the call's stream
+ * (hipFreeAsync / hipMallocAsync: no device synchronisation), so device entry
+ * points stay enqueue-only either way; cda_reserve just moves the allocations
+ * out of the first calls. */
 int cda_reserve(cda_ctx *ctx, uint32_t k, uint32_t n);
 
 /* As cda_extend_dah_device, but the k*k ODS shares are already in place in
@@ -210,7 +212,7 @@ int cda_split_combine(cda_ctx *ctx, const void *d_row_subtree_slots, uint32_t pa
  *   d_row_roots / d_col_roots (W*90) / d_data_root (32): rank 0 only;
  *   d_err: one device uint32, on rank 0 the MIN over ranks of the push-order
  *     words (0xFFFFFFFF = ordered; axis<<24 | index<<12 | position; 0 = a rank
- *     failed locally and the outputs are invalid). */
+ *     failed locally: rank 0 then returns CDA_ERR_DEVICE and writes no roots). */
 #define CDA_COMM_ID_BYTES 128
 int cda_comm_unique_id(uint8_t id[CDA_COMM_ID_BYTES]);
 int cda_comm_init(cda_ctx *ctx, int rank, int world, const uint8_t id[CDA_COMM_ID_BYTES]);
@@ -222,10 +224,13 @@ int cda_comm_destroy(cda_ctx *ctx);
  * every rank before any collective; scratch is sized when k changes, followed
  * by one agreement all-reduce, so an allocation failure on any rank makes
  * every rank return CDA_ERR_OOM; a local failure after that keeps the rank in
- * the remaining collectives with its push-order word poisoned to 0 (rank 0's
- * reduced d_err is then 0: the outputs are invalid) and returns the rank's
- * error; a failed RCCL call closes its group, aborts the communicator and
- * returns CDA_ERR_COMM. */
+ * the remaining collectives with its push-order word poisoned to 0 and returns
+ * the rank's error; rank 0 reads the reduced word back and, when it is 0 (a
+ * peer failed), returns CDA_ERR_DEVICE without writing roots; a failed RCCL
+ * call closes its group, aborts the communicator and returns CDA_ERR_COMM, and
+ * so does a call that cda_comm_abort released while it waited in a collective
+ * (every RCCL post re-reads the communicator under a lock that the abort also
+ * takes, so no call touches an aborted communicator). */
 int cda_comm_abort(cda_ctx *ctx);
 int cda_extend_dah_split(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, void *d_col_block, void *d_row_roots,
                          void *d_col_roots, void *d_data_root, uint32_t *d_err, void *stream);
