@@ -114,14 +114,16 @@ hipError_t launch_level(const Forest* f, uint32_t n_forest, uint32_t n_in, uint3
 hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t top, uint32_t n_squares,
                            hipStream_t stream);
 // Every remaining level of up to two forests of n_in (<= 256) nodes per tree
-// in one launch (a workgroup takes 256 / n_in trees, levels in LDS); the roots go to
+// in one launch (a workgroup takes 256 / n_in trees, levels in LDS; wide: 8 <=
+// n_in <= 512, 512 / n_in trees, the first level a thread per parent, the
+// rest lane pairs -- for a first level too wide for lane pairs); the roots go to
 // roots / root_slots as in launch_level, and if dig is non-NULL the first
 // levels of the data root over the n_items roots per square: RFC-6962 leaf
 // digests and, where every workgroup holds a power-of-two group of roots,
 // inner levels over the group; *n_dig_out (<= n_items) digests per square go
 // to dig[sq][.] for launch_data_root_digests.
 hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n_squares, uint32_t* dig,
-                           uint32_t n_items, hipStream_t stream, uint32_t* n_dig_out = nullptr);
+                           uint32_t n_items, hipStream_t stream, uint32_t* n_dig_out = nullptr, bool wide = false);
 // RFC-6962 data root over n_items 96-B root slots per square (power of two).
 hipError_t launch_data_root(const uint8_t* root_slots, uint32_t n_items, uint32_t n_squares, uint8_t* data_roots,
                             hipStream_t stream);

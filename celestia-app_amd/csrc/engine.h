@@ -255,8 +255,9 @@ class Engine {
                     bool subtrees = false);
     int subtree_min_ = 8;   // CDA_SUBTREE: fused subtree levels of >= this many leaves (0 = off)
     uint64_t subtree_lanes_ = 0;   // CDA_SUBTREE_LANES: lanes a subtree launch must hold (0 = by tree size)
-    uint32_t top_fuse_nodes(uint32_t W, uint32_t n) const;
+    uint32_t top_fuse_nodes(uint32_t W, uint32_t n, bool* wide = nullptr) const;
     int top_fuse_ = -1;   // CDA_TOP_FUSE (tuning / A-B): -1 auto, 0 off, N = nodes per tree
+    int top_wide_ = 2;    // CDA_TOP_WIDE: levels the tree top absorbs below the lane-pair level
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,
                          bool src_is_eds);
 
@@ -280,15 +281,13 @@ class Engine {
     hipStream_t copy_out_ = nullptr;
     hipEvent_t ev_rs_ = nullptr, ev_out_ = nullptr;
     int enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
-                           hipEvent_t ready, hipEvent_t done, hipStream_t q1 = nullptr, hipEvent_t q1_done = nullptr);
+                           hipEvent_t ready, hipEvent_t done);
     // Big host-buffer batches (host_extend_dah, n > 2 chunks): chunks of
     // squares through a ring of kPipeSlots device slots, H2D on copy_in_,
     // extension + hashing on stream_, parity D2H on copy_out_, so chunk i+1
     // goes up while chunk i computes and chunk i-1 comes down.
     static constexpr uint32_t kPipeSlots = 3;
-    hipStream_t copy_in_ = nullptr, copy_q1_ = nullptr;
-    hipEvent_t pipe_q1_[kPipeSlots] = {};
-    bool host_d2h2_ = true;   // CDA_HOST_D2H2: the 2-D Q1 copies on their own stream (A/B)
+    hipStream_t copy_in_ = nullptr;
     hipEvent_t pipe_in_[kPipeSlots] = {}, pipe_rs_[kPipeSlots] = {}, pipe_d2h_[kPipeSlots] = {},
                pipe_comp_[kPipeSlots] = {};
     uint32_t host_pipe_chunk_ = 0;   // CDA_HOST_PIPE_CHUNK: squares per chunk (0 = auto: ~256 MiB of ODS)

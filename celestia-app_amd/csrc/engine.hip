@@ -101,11 +101,10 @@ Engine::~Engine() {
     if (order_ev_) (void)hipEventDestroy(order_ev_);
     if (ev_rs_) (void)hipEventDestroy(ev_rs_);
     if (ev_out_) (void)hipEventDestroy(ev_out_);
-    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_, pipe_q1_})
+    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
         for (uint32_t i = 0; i < kPipeSlots; i++)
             if (e[i]) (void)hipEventDestroy(e[i]);
     if (copy_in_) (void)hipStreamDestroy(copy_in_);
-    if (copy_q1_) (void)hipStreamDestroy(copy_q1_);
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
@@ -189,9 +188,7 @@ int Engine::init() {
     if ((rc = check(hipEventCreateWithFlags(&ev_rs_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     if ((rc = check(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming), "hipEventCreate"))) return rc;
     if ((rc = check(hipStreamCreateWithFlags(&copy_in_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
-    if ((rc = check(hipStreamCreateWithFlags(&copy_q1_, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
-    if (const char* env = getenv("CDA_HOST_D2H2")) host_d2h2_ = atoi(env) != 0;
-    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_, pipe_q1_})
+    for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
         for (uint32_t i = 0; i < kPipeSlots; i++)
             if ((rc = check(hipEventCreateWithFlags(&e[i], hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
@@ -209,6 +206,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
+    if (const char* env = getenv("CDA_TOP_WIDE")) top_wide_ = atoi(env);
     if (const char* env = getenv("CDA_SUBTREE")) subtree_min_ = atoi(env);
     if (const char* env = getenv("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
@@ -236,11 +234,26 @@ static bool pow2(uint64_t x) { return x && !(x & (x - 1)); }
 // Nodes per tree at which the NMT levels switch from one wide launch per level
 // to tree_top_kernel (0 = never): the first level whose parents, over all 2W
 // trees of the n squares, fill less than one wave per SIMD of the chip
-// (1024 SIMDs x 64 lanes).  CDA_TOP_FUSE=0 disables, =N forces N.
-uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n) const {
+// (1024 SIMDs x 64 lanes) -- lane pairs from there -- and then up to
+// top_wide_ (CDA_TOP_WIDE) levels more, while the lane pairs of the level
+// below the first fit in two waves per SIMD: the first of them runs a thread
+// per parent inside the tree top (*wide), which saves their per-level
+// launches (drain tail + boundary each).  CDA_TOP_FUSE=0 disables, =N forces
+// N (not wide).
+uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n, bool* wide) const {
+    if (wide) *wide = false;
     if (top_fuse_ >= 0) return (uint32_t)top_fuse_ <= W && top_fuse_ <= 256 ? (uint32_t)top_fuse_ : 0;
-    for (uint32_t m = W; m >= 2; m /= 2)
-        if ((uint64_t)n * 2 * W * (m / 2) < 65536) return m <= 256 ? m : 0;
+    for (uint32_t m = W; m >= 2; m /= 2) {
+        if ((uint64_t)n * 2 * W * (m / 2) >= 65536) continue;
+        if (m > 256) return 0;
+        uint32_t t = m;
+        for (int e = 0; e < top_wide_ && 2 * t <= W && 2 * t <= 512 && 2 * t >= 8 &&
+                        2 * (uint64_t)n * 2 * W * (t / 2) <= 131072;
+             e++)
+            t *= 2;
+        if (wide) *wide = t > m;
+        return t;
+    }
     return 0;
 }
 
@@ -488,9 +501,13 @@ int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const
     // parents; the latency-bound rest of the trees (and the data root's RFC
     // leaf digests) in one tree_top_kernel launch.
     // (from == 1: the chunks already produced the roots -- no tree top)
-    uint32_t top = from > 1 ? top_fuse_nodes(W, n) : 0;
+    bool wide = false;
+    uint32_t top = from > 1 ? top_fuse_nodes(W, n, &wide) : 0;
     uint32_t n_dig = 2 * W;   // digests per square the tree top leaves for the data root
-    if (top > from) top = from;
+    if (top > from) {
+        top = from;
+        wide = false;
+    }
     if (from > 1) {
         const uint32_t stop = top ? top : 1;
         mark_begin(kStageLevels, s);
@@ -502,7 +519,7 @@ int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const
             const uint64_t off[2] = {0, slots_sq / 2};
             if ((rc = run_forests(f, 2, from, n, a, b, slots_sq, off, s, stop))) return rc;
         }
-        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig : nullptr, 2 * W, s, &n_dig),
+        if (top && (rc = check(launch_tree_top(f, 2, top, n, d_roots ? dig : nullptr, 2 * W, s, &n_dig, wide),
                                "nmt tree top")))
             return rc;
         mark_end(s);
@@ -871,7 +888,7 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
 }
 
 int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
-                               hipEvent_t ready, hipEvent_t done, hipStream_t q1, hipEvent_t q1_done) {
+                               hipEvent_t ready, hipEvent_t done) {
     const size_t W = 2 * (size_t)k, sq_b = W * W * kShare, half = k * W * kShare;
     int rc;
     if ((rc = check(hipEventRecord(ready, from), "hipEventRecord"))) return rc;
@@ -880,23 +897,18 @@ int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uin
         if ((rc = check(hipMemcpyAsync(eds, d_eds, n * sq_b, hipMemcpyDeviceToHost, copy_out_), "D2H EDS"))) return rc;
         return check(hipEventRecord(done, copy_out_), "hipEventRecord");
     }
-    // Q1 (rows 0..k-1, columns k..2k-1: strided) as 2-D copies -- on stream q1
-    // when given, so they run beside the linear Q2|Q3 copies
-    hipStream_t sq1 = q1 ? q1 : copy_out_;
-    if (q1 && (rc = check(hipStreamWaitEvent(q1, ready, 0), "hipStreamWaitEvent"))) return rc;
+    // Q1 (rows 0..k-1, columns k..2k-1: strided) as 2-D copies, Q2|Q3 (rows
+    // k..2k-1) linear (a second stream for the Q1 copies measured no faster:
+    // profiles/r04/host_d2h_streams.txt)
     for (uint32_t sq = 0; sq < n; sq++) {
         if ((rc = check(hipMemcpy2DAsync(eds + sq * sq_b + k * kShare, W * kShare, d_eds + sq * sq_b + k * kShare,
-                                         W * kShare, (size_t)k * kShare, k, hipMemcpyDeviceToHost, sq1),
+                                         W * kShare, (size_t)k * kShare, k, hipMemcpyDeviceToHost, copy_out_),
                         "D2H Q1")))
             return rc;
         if ((rc = check(hipMemcpyAsync(eds + sq * sq_b + half, d_eds + sq * sq_b + half, half, hipMemcpyDeviceToHost,
                                        copy_out_),
                         "D2H Q2|Q3")))
             return rc;
-    }
-    if (q1) {
-        if ((rc = check(hipEventRecord(q1_done, q1), "hipEventRecord"))) return rc;
-        if ((rc = check(hipStreamWaitEvent(copy_out_, q1_done, 0), "hipStreamWaitEvent"))) return rc;
     }
     return check(hipEventRecord(done, copy_out_), "hipEventRecord");
 }
@@ -944,8 +956,7 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
         if (eds && i >= kPipeSlots && (rc = check(hipStreamWaitEvent(s, pipe_d2h_[slot], 0), "hipStreamWaitEvent")))
             return rc;
         if ((rc = enqueue_extend(d_ods, k, m, d_eds, s, err + i0))) return rc;
-        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * eds_sq, s, pipe_rs_[slot], pipe_d2h_[slot],
-                                            host_d2h2_ ? copy_q1_ : nullptr, pipe_q1_[slot])))
+        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * eds_sq, s, pipe_rs_[slot], pipe_d2h_[slot])))
             return rc;
         if ((rc = enqueue_dah(d_eds, k, m, h_rows_.as<uint8_t>() + i0 * root_sq, h_cols_.as<uint8_t>() + i0 * root_sq,
                               h_roots_.as<uint8_t>() + (size_t)i0 * 32, err + i0, nullptr, s, true)))

@@ -321,11 +321,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEVEL_W
 // 64 consecutive trees of one subtree index, so the parity mid-state branch
 // of hash_node stays uniform.
 // ---------------------------------------------------------------------------
-#ifndef CDA_SUBTREE_WPE   // experiment (r04): waves per SIMD the subtree kernel is register-sized for
-#define CDA_SUBTREE_WPE 3
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_SUBTREE_WPE))) void subtree_kernel(const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx,
-                                                      uint32_t nsq, uint32_t nblocks) {
+// (Register-sized for 4 waves per SIMD -- 128 VGPRs, a few spills -- where a
+// launch holds between 3 and 4 waves per SIMD, e.g. config 4's 128-square
+// shard: 2 % slower in an interleaved A/B, profiles/r04/
+// r04o_fused_root_wide_subtree4_ab.txt; tools/probes/top_root_fused_subtree4.patch.)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void subtree_kernel(
+    const Forest2 fs, uint32_t n_in, uint32_t slog, uint32_t nbx, uint32_t nsq, uint32_t nblocks) {
     const uint32_t S = 1u << slog;
     const uint32_t top = n_in >> slog;   // subtree roots per tree
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
@@ -391,254 +392,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_SUBTREE
             store_slot(out + ((size_t)t * top + s) * kSlot, cur);
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-// Fused top of the trees (latency-bound part: fewer parents than the chip has
-// wave slots).  One workgroup takes tpw trees and runs every remaining level
-// in LDS, no launch per level: the first level reads the trees' input slots
-// from global memory, later levels ping-pong between two LDS halves.  The
-// root goes out packed (90 B) and as a 96-B slot like level_kernel's.  If
-// dig is set, the workgroup also starts the data root: the RFC-6962 leaf
-// digests of its tpw roots (consecutive items of rowRoots || colRoots) and
-// `rfc_levels` inner levels over them, one digest per 2^rfc_levels roots to
-// dig[sq][item >> rfc_levels] -- the data root's throughput-heavy first levels
-// spread over all workgroups instead of one per square.  PAIR: a lane pair
-// per parent (kTopThreads pairs).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kTopThreads = 128;   // parents per workgroup: tpw = 256 / n_in trees x n_in / 2
-
-template <bool PAIR>
-__global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top_kernel(
-    const Forest2 fs, uint32_t n_in, uint32_t tpw, uint32_t* __restrict__ dig, uint32_t n_dig, uint32_t rfc_levels,
-    uint32_t helpers) {
-    __shared__ __attribute__((aligned(16))) uint32_t buf[2][kTopThreads][kSlotWords];
-    // schedule helpers (PAIR, levels of <= 64 parents): K + W of blocks 1 and
-    // 2 of unit u's node at kwb[u][block - 1][t] (rows padded 4 words so the
-    // units' 16-B reads spread over the banks)
-    constexpr uint32_t kKwRow = 2 * 64 + 4;
-    __shared__ __attribute__((aligned(16))) uint32_t kwb[PAIR ? 64 : 1][kKwRow];
-    const size_t sq = blockIdx.y;
-    const uint32_t n_trees = fs.f[0].n_trees + fs.f[1].n_trees;
-    const uint32_t u = PAIR ? threadIdx.x >> 1 : threadIdx.x;   // unit (parent) index
-    const bool A = PAIR && (threadIdx.x & 1);
-    const bool writer = !A;                                    // one store per unit
-    uint32_t o[kSlotWords];
-    uint32_t cur = 0;
-    for (uint32_t m = n_in; m >= 2; m /= 2) {
-        const uint32_t half = m / 2;
-        const uint32_t j = u / half, p = u % half;   // tree j of this workgroup, parent p
-        const uint32_t g = blockIdx.x * tpw + j;
-        if (PAIR && helpers && m < n_in && tpw * half <= 64) {
-            // At most two waves of parents: waves 2 and 3 would idle, so they
-            // compute the message schedules of blocks 1 and 2 of every node
-            // (one lane per block) while waves 0-1 run block 0; the parents'
-            // lane pairs then run blocks 1 and 2 rounds-only (sha_pair_compress_kw:
-            // the chain of dependent compressions is the critical wave's
-            // instruction count, DESIGN.md 3.5).
-            Sha<true> h;
-            const bool work = threadIdx.x < 128 && j < tpw && g < n_trees;
-            uint32_t L[kSlotWords], R[kSlotWords];
-            if (threadIdx.x >= 128) {
-                const uint32_t hi = threadIdx.x - 128, hu = hi >> 1, hb = 1 + (hi & 1);
-                const uint32_t hj = hu / half, hp = hu % half;
-                if (hj < tpw && blockIdx.x * tpw + hj < n_trees) {
-#pragma unroll
-                    for (int i = 0; i < kSlotWords; i++) {
-                        L[i] = bswap32(buf[cur][hj * m + 2 * hp][i]);
-                        R[i] = bswap32(buf[cur][hj * m + 2 * hp + 1][i]);
-                    }
-                    // the block index must be a compile-time constant in
-                    // node_msg (a run-time one indexes L / R dynamically:
-                    // private memory)
-                    uint32_t w[16];
-                    if (hb == 1) {
-#pragma unroll
-                        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 + i);
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 32 + i);
-                    }
-                    sha_schedule_kw(w, &kwb[hu][64 * (hb - 1)]);
-                }
-            } else if (work) {
-#pragma unroll
-                for (int i = 0; i < kSlotWords; i++) {
-                    L[i] = bswap32(buf[cur][j * m + 2 * p][i]);
-                    R[i] = bswap32(buf[cur][j * m + 2 * p + 1][i]);
-                }
-                h.init(A);
-                uint32_t w[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, i);
-                h.compress(w, A);
-            }
-            __syncthreads();   // the helpers' schedules are in kwb
-            if (work) {
-#pragma unroll
-                for (int b = 0; b < 2; b++) {
-                    uint4 kw[16];
-                    const uint4* row = reinterpret_cast<const uint4*>(&kwb[u][64 * b]);
-#pragma unroll
-                    for (int q = 0; q < 16; q++) kw[q] = row[q];
-                    sha_pair_compress_kw(h.st, kw, A);
-                }
-                uint32_t D[8];
-                h.digest(A, D);
-                inner_node_words(L, R, D, o);
-                if (m > 2 && writer) {
-#pragma unroll
-                    for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][u][i] = o[i];
-                }
-            }
-        } else if (j < tpw && g < n_trees) {
-            uint32_t L[kSlotWords], R[kSlotWords];
-            if (m == n_in) {
-                const bool f1 = g >= fs.f[0].n_trees;
-                const Forest& F = fs.f[f1 ? 1 : 0];
-                const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
-                const uint8_t* l =
-                    F.in + sq * F.in_sq + ((size_t)t * F.tree_stride + (size_t)(2 * p) * F.node_stride) * kSlot;
-                load_slot_be(l, L);
-                load_slot_be(l + (size_t)F.node_stride * kSlot, R);
-            } else {
-#pragma unroll
-                for (int i = 0; i < kSlotWords; i++) {
-                    L[i] = bswap32(buf[cur][j * m + 2 * p][i]);
-                    R[i] = bswap32(buf[cur][j * m + 2 * p + 1][i]);
-                }
-            }
-            hash_node_u<PAIR>(L, R, o, A);
-            if (m > 2 && writer) {
-#pragma unroll
-                for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][u][i] = o[i];
-            }
-        }
-        __syncthreads();
-        cur ^= 1;
-    }
-    // unit j < tpw holds tree j's root slot in o
-    const uint32_t g = blockIdx.x * tpw + u;
-    const bool has = u < tpw && g < n_trees;
-    uint32_t D[8];
-    if (has) {
-        const bool f1 = g >= fs.f[0].n_trees;
-        const Forest& F = fs.f[f1 ? 1 : 0];
-        const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
-        if (writer && F.roots) {
-            uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
-#pragma unroll
-            for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
-        }
-        if (writer && F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
-        if (dig) {
-            uint32_t I[kSlotWords];
-#pragma unroll
-            for (int i = 0; i < kSlotWords; i++) I[i] = bswap32(o[i]);
-            rfc_leaf_u<PAIR>(I, D, A);
-        }
-    }
-    if (!dig) return;
-    // rfc_levels inner levels over this workgroup's tpw digests (the host only
-    // asks for them when every workgroup holds tpw trees): unit u < cnt holds
-    // digest u of the current level
-    uint32_t* dl = &buf[0][0][0];   // [unit][8]
-    uint32_t cnt = tpw;
-    for (uint32_t lv = 0; lv < rfc_levels; lv++) {
-        if (u < cnt && writer) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) dl[u * 8 + i] = D[i];
-        }
-        __syncthreads();
-        cnt /= 2;
-        if (u < cnt) {
-            uint32_t a[8], b[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                a[i] = dl[(2 * u) * 8 + i];
-                b[i] = dl[(2 * u + 1) * 8 + i];
-            }
-            rfc_inner_u<PAIR>(a, b, D, A);
-        }
-        __syncthreads();
-    }
-    if (has && writer && u < cnt) {
-        uint4* d = reinterpret_cast<uint4*>(dig + (sq * n_dig + ((blockIdx.x * tpw) >> rfc_levels) + u) * 8);
-        d[0] = make_uint4(D[0], D[1], D[2], D[3]);
-        d[1] = make_uint4(D[4], D[5], D[6], D[7]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Data root: RFC-6962 over the 2W root slots (rows then columns); 2W is a
-// power of two so the tree is perfect.  One 256-thread block per square.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void data_root_kernel(const uint8_t* __restrict__ root_slots, uint32_t n,
-                                                       uint8_t* __restrict__ data_roots) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // ping [n][8] | pong [n/2][8]
-    const size_t sq = blockIdx.x;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        uint32_t I[kSlotWords], w[16];
-        load_slot_be(root_slots + (sq * n + i) * (size_t)kSlot, I);
-        ShaState st;
-        sha_init(st);
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-#pragma unroll
-            for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
-            sha_compress(st, w);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) hs[i * 8 + j] = st.h[j];
-    }
-    __syncthreads();
-    uint32_t* src = hs;
-    uint32_t* dst = hs + n * 8;
-    for (uint32_t m = n / 2; m >= 1; m >>= 1) {
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-            uint32_t A[8], B[8], w[16];
-#pragma unroll
-            for (int j = 0; j < 8; j++) { A[j] = src[(2 * i) * 8 + j]; B[j] = src[(2 * i + 1) * 8 + j]; }
-            ShaState st;
-            sha_init(st);
-#pragma unroll
-            for (int b = 0; b < 2; b++) {
-#pragma unroll
-                for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(A, B, 16 * b + j);
-                sha_compress(st, w);
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) dst[i * 8 + j] = st.h[j];
-        }
-        __syncthreads();
-        uint32_t* t = src; src = dst; dst = t;
-    }
-    if (threadIdx.x == 0) {
-        uint32_t* o = reinterpret_cast<uint32_t*>(data_roots + sq * 32);
-#pragma unroll
-        for (int j = 0; j < 8; j++) o[j] = bswap32(src[j]);
-    }
-}
-
-// RFC-6962 leaf digests sha256(0x00 || root) of n 96-B root slots (one thread
-// each, 2 compressions), 8 big-endian-valued words per digest.
-__global__ __launch_bounds__(256) void rfc_leaf_kernel(const uint8_t* __restrict__ slots, uint32_t n,
-                                                      uint32_t* __restrict__ dig) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    uint32_t I[kSlotWords], w[16];
-    load_slot_be(slots + (size_t)i * kSlot, I);
-    ShaState st;
-    sha_init(st);
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
-        sha_compress(st, w);
-    }
-    uint4* d = reinterpret_cast<uint4*>(dig + (size_t)i * 8);
-    d[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
-    d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
 }
 
 // Data root from n leaf digests (rfc_leaf_kernel, or the group digests of
@@ -802,16 +555,18 @@ __device__ __forceinline__ void data_root_level_helped(const uint32_t* __restric
     }
 }
 
-__global__ __launch_bounds__(512) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
-                                                               uint8_t* __restrict__ data_roots,
-                                                               const uint32_t* __restrict__ err,
-                                                               int32_t* __restrict__ status, uint32_t pair_ok) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [n/2][8] | [n/4][8]
-    __shared__ __attribute__((aligned(16))) uint32_t kwb[32][kDrKwRow];   // schedule helpers' K + W
-    const size_t sq = blockIdx.x;
-    const uint32_t* D = dig + sq * (size_t)n * 8;
-    uint32_t* src = hs;
-    uint32_t* dst = hs + (n / 2) * 8;
+// The data root's inner levels over the n digests at D (global memory, or
+// LDS in the fused tree top): the first level writes src, later levels
+// ping-pong src / dst (LDS, room for n/2 and n/4 digests; dst may be D's LDS
+// once the first level has read it).  A level of m <= 128 parents (at most a
+// wave per SIMD of lane pairs) runs a lane pair per parent, wider levels a
+// thread per parent; pair_ok == 2: schedule helpers in levels of <= 32
+// parents.  Thread 0 writes the square's data root and its push-order status
+// (status_kernel, fused: one launch less).  Every thread of the workgroup
+// calls this (barriers).
+__device__ __forceinline__ void data_root_levels(const uint32_t* D, uint32_t n, uint32_t* src, uint32_t* dst,
+                                                 uint32_t (*kwb)[kDrKwRow], uint32_t pair_ok, uint8_t* data_root,
+                                                 const uint32_t* err, int32_t* status) {
     for (uint32_t m = n / 2; m >= 1; m >>= 1) {
         const uint32_t* in = m == n / 2 ? D : src;
         uint32_t* out = m == n / 2 ? src : dst;
@@ -823,16 +578,307 @@ __global__ __launch_bounds__(512) void data_root_digest_kernel(const uint32_t* _
             data_root_level<false>(in, out, m);
         __syncthreads();
         if (m != n / 2) {
-            uint32_t* t = src; src = dst; dst = t;
+            uint32_t* t = src;
+            src = dst;
+            dst = t;
         }
+    }
+    if (threadIdx.x == 0) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(data_root);
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = bswap32(src[j]);
+        if (status) *status = *err == 0xFFFFFFFFu ? 0 : -3;   // CDA_OK / CDA_ERR_PUSH_ORDER
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused top of the trees (latency-bound part: fewer parents than the chip has
+// wave slots).  One workgroup takes tpw trees and runs every remaining level
+// in LDS, no launch per level: the first level reads the trees' input slots
+// from global memory, later levels ping-pong between two LDS halves.  The
+// root goes out packed (90 B) and as a 96-B slot like level_kernel's.  If
+// dig is set, the workgroup also starts the data root: the RFC-6962 leaf
+// digests of its tpw roots (consecutive items of rowRoots || colRoots) and
+// `rfc_levels` inner levels over them, one digest per 2^rfc_levels roots to
+// dig[sq][item >> rfc_levels] -- the data root's throughput-heavy first levels
+// spread over all workgroups instead of one per square.  PAIR: a lane pair
+// per parent (kTopThreads pairs).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kTopThreads = 128;   // parents per workgroup: tpw = 256 / n_in trees x n_in / 2
+
+// flags: kTopHelpers -- schedule-helper waves in the narrow levels (PAIR);
+// kTopWide -- the first level runs a thread per parent over 2 kTopThreads
+// parents (tpw = 4 kTopThreads / n_in trees), the rest as lane pairs: one
+// launch covers a level that has more parents than the lane pairs fit in a
+// wave per SIMD (n_in >= 8).
+constexpr uint32_t kTopHelpers = 1, kTopWide = 2;
+template <bool PAIR>
+__global__ __launch_bounds__(PAIR ? 2 * kTopThreads : kTopThreads) void tree_top_kernel(
+    const Forest2 fs, uint32_t n_in, uint32_t tpw, uint32_t* __restrict__ dig, uint32_t n_dig, uint32_t rfc_levels,
+    uint32_t flags) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[2][kTopThreads][kSlotWords];
+    // schedule helpers (PAIR, levels of <= 64 parents): K + W of blocks 1 and
+    // 2 of unit u's node at kwb[u][block - 1][t] (rows padded 4 words so the
+    // units' 16-B reads spread over the banks)
+    constexpr uint32_t kKwRow = 2 * 64 + 4;
+    __shared__ __attribute__((aligned(16))) uint32_t kwb[PAIR ? 64 : 1][kKwRow];
+    // kTopWide: the first level's 2 kTopThreads nodes, in kwb (the second
+    // level has 128 parents, no helpers: kwb is free until the third)
+    static_assert(!PAIR || 64 * kKwRow >= 2 * kTopThreads * kSlotWords, "wide level output must fit in kwb");
+    uint32_t* wide_out = &kwb[0][0];
+    const bool helpers = flags & kTopHelpers;
+    const bool wide = PAIR && (flags & kTopWide);
+    const size_t sq = blockIdx.y;
+    const uint32_t n_trees = fs.f[0].n_trees + fs.f[1].n_trees;
+    const uint32_t u = PAIR ? threadIdx.x >> 1 : threadIdx.x;   // unit (parent) index
+    const bool A = PAIR && (threadIdx.x & 1);
+    const bool writer = !A;                                    // one store per unit
+    uint32_t o[kSlotWords];
+    uint32_t cur = 0;
+    if (wide) {   // first level: a thread per parent, from global memory into wide_out
+        const uint32_t half = n_in / 2, j = threadIdx.x / half, p = threadIdx.x % half;
+        const uint32_t g = blockIdx.x * tpw + j;
+        if (j < tpw && g < n_trees) {
+            const bool f1 = g >= fs.f[0].n_trees;
+            const Forest& F = fs.f[f1 ? 1 : 0];
+            const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
+            const uint8_t* l = F.in + sq * F.in_sq + ((size_t)t * F.tree_stride + (size_t)(2 * p) * F.node_stride) * kSlot;
+            uint32_t L[kSlotWords], R[kSlotWords], w1[kSlotWords];
+            load_slot_be(l, L);
+            load_slot_be(l + (size_t)F.node_stride * kSlot, R);
+            hash_node_u<false>(L, R, w1, false);
+#pragma unroll
+            for (int i = 0; i < kSlotWords; i++) wide_out[threadIdx.x * kSlotWords + i] = w1[i];
+        }
+        __syncthreads();
+    }
+    for (uint32_t m = wide ? n_in / 2 : n_in; m >= 2; m /= 2) {
+        const uint32_t half = m / 2;
+        const uint32_t j = u / half, p = u % half;   // tree j of this workgroup, parent p
+        const uint32_t g = blockIdx.x * tpw + j;
+        // this level's input nodes: node q of tree j at in_lds[(j * m + q) * kSlotWords]
+        const uint32_t* in_lds = wide && m == n_in / 2 ? wide_out : &buf[cur][0][0];
+        if (PAIR && helpers && m < n_in && tpw * half <= 64) {
+            // At most two waves of parents: waves 2 and 3 would idle, so they
+            // compute the message schedules of blocks 1 and 2 of every node
+            // (one lane per block) while waves 0-1 run block 0; the parents'
+            // lane pairs then run blocks 1 and 2 rounds-only (sha_pair_compress_kw:
+            // the chain of dependent compressions is the critical wave's
+            // instruction count, DESIGN.md 3.5).
+            Sha<true> h;
+            const bool work = threadIdx.x < 128 && j < tpw && g < n_trees;
+            uint32_t L[kSlotWords], R[kSlotWords];
+            if (threadIdx.x >= 128) {
+                const uint32_t hi = threadIdx.x - 128, hu = hi >> 1, hb = 1 + (hi & 1);
+                const uint32_t hj = hu / half, hp = hu % half;
+                if (hj < tpw && blockIdx.x * tpw + hj < n_trees) {
+#pragma unroll
+                    for (int i = 0; i < kSlotWords; i++) {
+                        L[i] = bswap32(in_lds[(hj * m + 2 * hp) * kSlotWords + i]);
+                        R[i] = bswap32(in_lds[(hj * m + 2 * hp + 1) * kSlotWords + i]);
+                    }
+                    // the block index must be a compile-time constant in
+                    // node_msg (a run-time one indexes L / R dynamically:
+                    // private memory)
+                    uint32_t w[16];
+                    if (hb == 1) {
+#pragma unroll
+                        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 16 + i);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, 32 + i);
+                    }
+                    sha_schedule_kw(w, &kwb[hu][64 * (hb - 1)]);
+                }
+            } else if (work) {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) {
+                    L[i] = bswap32(in_lds[(j * m + 2 * p) * kSlotWords + i]);
+                    R[i] = bswap32(in_lds[(j * m + 2 * p + 1) * kSlotWords + i]);
+                }
+                h.init(A);
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) w[i] = node_msg(L, R, i);
+                h.compress(w, A);
+            }
+            __syncthreads();   // the helpers' schedules are in kwb
+            if (work) {
+#pragma unroll
+                for (int b = 0; b < 2; b++) {
+                    uint4 kw[16];
+                    const uint4* row = reinterpret_cast<const uint4*>(&kwb[u][64 * b]);
+#pragma unroll
+                    for (int q = 0; q < 16; q++) kw[q] = row[q];
+                    sha_pair_compress_kw(h.st, kw, A);
+                }
+                uint32_t D[8];
+                h.digest(A, D);
+                inner_node_words(L, R, D, o);
+                if (m > 2 && writer) {
+#pragma unroll
+                    for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][u][i] = o[i];
+                }
+            }
+        } else if (j < tpw && g < n_trees) {
+            uint32_t L[kSlotWords], R[kSlotWords];
+            if (m == n_in) {
+                const bool f1 = g >= fs.f[0].n_trees;
+                const Forest& F = fs.f[f1 ? 1 : 0];
+                const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
+                const uint8_t* l =
+                    F.in + sq * F.in_sq + ((size_t)t * F.tree_stride + (size_t)(2 * p) * F.node_stride) * kSlot;
+                load_slot_be(l, L);
+                load_slot_be(l + (size_t)F.node_stride * kSlot, R);
+            } else {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) {
+                    L[i] = bswap32(in_lds[(j * m + 2 * p) * kSlotWords + i]);
+                    R[i] = bswap32(in_lds[(j * m + 2 * p + 1) * kSlotWords + i]);
+                }
+            }
+            hash_node_u<PAIR>(L, R, o, A);
+            if (m > 2 && writer) {
+#pragma unroll
+                for (int i = 0; i < kSlotWords; i++) buf[cur ^ 1][u][i] = o[i];
+            }
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    // unit j < tpw holds tree j's root slot in o
+    const uint32_t g = blockIdx.x * tpw + u;
+    const bool has = u < tpw && g < n_trees;
+    uint32_t D[8];
+    if (has) {
+        const bool f1 = g >= fs.f[0].n_trees;
+        const Forest& F = fs.f[f1 ? 1 : 0];
+        const uint32_t t = f1 ? g - fs.f[0].n_trees : g;
+        if (writer && F.roots) {
+            uint16_t* d16 = reinterpret_cast<uint16_t*>(F.roots + sq * F.roots_sq + (size_t)t * kNode);
+#pragma unroll
+            for (int i = 0; i < kNode / 2; i++) d16[i] = (uint16_t)(o[i / 2] >> (16 * (i & 1)));
+        }
+        if (writer && F.root_slots) store_slot(F.root_slots + sq * F.rslot_sq + (size_t)(F.root0 + t) * kSlot, o);
+        if (dig) {
+            uint32_t I[kSlotWords];
+#pragma unroll
+            for (int i = 0; i < kSlotWords; i++) I[i] = bswap32(o[i]);
+            rfc_leaf_u<PAIR>(I, D, A);
+        }
+    }
+    if (!dig) return;
+    // rfc_levels inner levels over this workgroup's tpw digests (the host only
+    // asks for them when every workgroup holds tpw trees): unit u < cnt holds
+    // digest u of the current level
+    uint32_t* dl = &buf[0][0][0];   // [unit][8]
+    uint32_t cnt = tpw;
+    for (uint32_t lv = 0; lv < rfc_levels; lv++) {
+        if (u < cnt && writer) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) dl[u * 8 + i] = D[i];
+        }
+        __syncthreads();
+        cnt /= 2;
+        if (u < cnt) {
+            uint32_t a[8], b[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                a[i] = dl[(2 * u) * 8 + i];
+                b[i] = dl[(2 * u + 1) * 8 + i];
+            }
+            rfc_inner_u<PAIR>(a, b, D, A);
+        }
+        __syncthreads();
+    }
+    if (has && writer && u < cnt) {
+        uint4* d = reinterpret_cast<uint4*>(dig + (sq * n_dig + ((blockIdx.x * tpw) >> rfc_levels) + u) * 8);
+        d[0] = make_uint4(D[0], D[1], D[2], D[3]);
+        d[1] = make_uint4(D[4], D[5], D[6], D[7]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Data root: RFC-6962 over the 2W root slots (rows then columns); 2W is a
+// power of two so the tree is perfect.  One 256-thread block per square.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void data_root_kernel(const uint8_t* __restrict__ root_slots, uint32_t n,
+                                                       uint8_t* __restrict__ data_roots) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // ping [n][8] | pong [n/2][8]
+    const size_t sq = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t I[kSlotWords], w[16];
+        load_slot_be(root_slots + (sq * n + i) * (size_t)kSlot, I);
+        ShaState st;
+        sha_init(st);
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
+            sha_compress(st, w);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) hs[i * 8 + j] = st.h[j];
+    }
+    __syncthreads();
+    uint32_t* src = hs;
+    uint32_t* dst = hs + n * 8;
+    for (uint32_t m = n / 2; m >= 1; m >>= 1) {
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            uint32_t A[8], B[8], w[16];
+#pragma unroll
+            for (int j = 0; j < 8; j++) { A[j] = src[(2 * i) * 8 + j]; B[j] = src[(2 * i + 1) * 8 + j]; }
+            ShaState st;
+            sha_init(st);
+#pragma unroll
+            for (int b = 0; b < 2; b++) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) w[j] = rfc_inner_msg(A, B, 16 * b + j);
+                sha_compress(st, w);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) dst[i * 8 + j] = st.h[j];
+        }
+        __syncthreads();
+        uint32_t* t = src; src = dst; dst = t;
     }
     if (threadIdx.x == 0) {
         uint32_t* o = reinterpret_cast<uint32_t*>(data_roots + sq * 32);
 #pragma unroll
         for (int j = 0; j < 8; j++) o[j] = bswap32(src[j]);
-        // the push-order status of the square (status_kernel, fused: one launch less)
-        if (status) status[sq] = err[sq] == 0xFFFFFFFFu ? 0 : -3;   // CDA_OK / CDA_ERR_PUSH_ORDER
     }
+}
+
+// RFC-6962 leaf digests sha256(0x00 || root) of n 96-B root slots (one thread
+// each, 2 compressions), 8 big-endian-valued words per digest.
+__global__ __launch_bounds__(256) void rfc_leaf_kernel(const uint8_t* __restrict__ slots, uint32_t n,
+                                                      uint32_t* __restrict__ dig) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t I[kSlotWords], w[16];
+    load_slot_be(slots + (size_t)i * kSlot, I);
+    ShaState st;
+    sha_init(st);
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = rfc_leaf_msg(I, 16 * b + j);
+        sha_compress(st, w);
+    }
+    uint4* d = reinterpret_cast<uint4*>(dig + (size_t)i * 8);
+    d[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+    d[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+}
+
+__global__ __launch_bounds__(512) void data_root_digest_kernel(const uint32_t* __restrict__ dig, uint32_t n,
+                                                               uint8_t* __restrict__ data_roots,
+                                                               const uint32_t* __restrict__ err,
+                                                               int32_t* __restrict__ status, uint32_t pair_ok) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hs[];   // [n/2][8] | [n/4][8]
+    __shared__ __attribute__((aligned(16))) uint32_t kwb[32][kDrKwRow];   // schedule helpers' K + W
+    const size_t sq = blockIdx.x;
+    data_root_levels(dig + sq * (size_t)n * 8, n, hs, hs + (n / 2) * 8, kwb, pair_ok, data_roots + sq * 32,
+                     err + sq, status ? status + sq : nullptr);
 }
 
 __global__ void status_kernel(const uint32_t* __restrict__ err, uint32_t n, int32_t* __restrict__ status) {
@@ -959,9 +1005,21 @@ static bool pair_sha_enabled() {
     return v;
 }
 
+// data_root_levels' mode: 0 a thread per parent, 1 lane pairs, 2 lane pairs +
+// schedule helpers (CDA_DR_HELPERS=0: no helpers; CDA_TOP_PAIR=0: no pairs)
+static uint32_t data_root_mode() {
+    static const bool dr_helpers = [] {
+        const char* e = getenv("CDA_DR_HELPERS");
+        return !(e && atoi(e) == 0);
+    }();
+    return pair_sha_enabled() ? (dr_helpers ? 2u : 1u) : 0u;
+}
+
 hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n, uint32_t* dig,
-                           uint32_t n_items, hipStream_t s, uint32_t* n_dig_out) {
-    if (n_forest < 1 || n_forest > 2 || n_in < 2 || n_in > 2 * kTopThreads || (n_in & (n_in - 1)))
+                           uint32_t n_items, hipStream_t s, uint32_t* n_dig_out, bool wide) {
+    wide = wide && pair_sha_enabled();
+    if (n_forest < 1 || n_forest > 2 || n_in < (wide ? 8u : 2u) || n_in > (wide ? 4 : 2) * kTopThreads ||
+        (n_in & (n_in - 1)))
         return hipErrorInvalidValue;
     Forest2 fs{};
     uint32_t trees = 0;
@@ -969,7 +1027,7 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
         fs.f[i] = f[i];
         trees += f[i].n_trees;
     }
-    const uint32_t tpw = 2 * kTopThreads / n_in;   // trees per workgroup
+    const uint32_t tpw = (wide ? 4 : 2) * kTopThreads / n_in;   // trees per workgroup
     // RFC-6962 levels inside the workgroups: while every workgroup holds tpw
     // of the n_items (a power of two) roots and at least 2 digests per square
     // remain for data_root_digest_kernel
@@ -983,18 +1041,19 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
     if (!rfc_in_top) lv = 0;
     const uint32_t n_dig = n_items >> lv;
     if (n_dig_out) *n_dig_out = n_dig;
-    // lane pairs while they still fit in a wave per SIMD (1024 SIMDs)
+    // lane pairs while they still fit in a wave per SIMD (1024 SIMDs); wide:
+    // the caller's choice (a thread per parent in the first level)
     const uint64_t parents = (uint64_t)n * trees * (n_in / 2);
-    const bool pair = pair_sha_enabled() && 2 * parents <= 65536;
+    const bool pair = wide || (pair_sha_enabled() && 2 * parents <= 65536);
     const dim3 grid((trees + tpw - 1) / tpw, n);
     // CDA_TOP_HELPERS=0 (A/B knob): no schedule-helper waves in the narrow levels
     static const uint32_t helpers = [] {
         const char* e = getenv("CDA_TOP_HELPERS");
-        return e && atoi(e) == 0 ? 0u : 1u;
+        return e && atoi(e) == 0 ? 0u : kTopHelpers;
     }();
     if (pair)
         hipLaunchKernelGGL(tree_top_kernel<true>, grid, dim3(2 * kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv,
-                           helpers);
+                           helpers | (wide ? kTopWide : 0u));
     else
         hipLaunchKernelGGL(tree_top_kernel<false>, grid, dim3(kTopThreads), 0, s, fs, n_in, tpw, dig, n_dig, lv, 0u);
     return hipGetLastError();
@@ -1044,12 +1103,7 @@ hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint3
     uint32_t threads = std::min<uint32_t>(n_items / 2, 512);
     threads = std::max<uint32_t>(threads, std::min<uint32_t>(n_items, 2 * kPairMaxParents));
     threads = std::max<uint32_t>((threads + 63) / 64 * 64, 64);
-    // CDA_DR_HELPERS=0 (A/B knob): no schedule helpers in the narrow data-root levels
-    static const bool dr_helpers = [] {
-        const char* e = getenv("CDA_DR_HELPERS");
-        return !(e && atoi(e) == 0);
-    }();
-    const uint32_t mode = pair_sha_enabled() ? (dr_helpers ? 2u : 1u) : 0u;
+    const uint32_t mode = data_root_mode();
     hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots,
                        status ? err : nullptr, status, mode);
     return hipGetLastError();

@@ -69,16 +69,6 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     constexpr int NW = 1 << (LOGK - 7);    // waves per workgroup
     constexpr int K = 1 << LOGK;
     rs_err_init(job);
-#ifdef CDA_BS16_STAGGER   // experiment: de-phase the first round's co-resident workgroups
-    {
-        const uint32_t id = blockIdx.y * gridDim.x + blockIdx.x;
-        if (id < 768) {
-            const uint32_t ph = (id / 256) % 3;
-            const uint64_t t0 = __builtin_amdgcn_s_memtime(), wait = (uint64_t)ph * CDA_BS16_STAGGER * 2200;
-            while (__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(127);
-        }
-    }
-#endif
     extern __shared__ u32x4 X[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, b4 = lane & 3, jl = lane >> 2;
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -10,8 +10,10 @@ for b in 128 1024; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r04i/prof_b$b -o b$b -- python3 $GRAFT_REPO_ROOT/bench.py --batch $b --no-extras --no-cpu --steps 5 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/r04i/prof_b$b.log 2>&1
 done
 cd $GRAFT_REPO_ROOT
+CDA_LIB=$PWD/celestia-app_amd/build_var/wfold/libcda.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "gf16 or k512 or codec_encode" > gpurun_out/r04i/wfold_parity.log 2>&1
+tail -2 gpurun_out/r04i/wfold_parity.log
 for rep in 1 2; do
-for v in prod stag20 stag35; do
+for v in prod stag20 stag35 wfold; do
   L=$PWD/celestia-app_amd/libcda.so
   [ $v != prod ] && L=$PWD/celestia-app_amd/build_var/$v/libcda.so
   for b in 1 4; do
