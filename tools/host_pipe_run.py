@@ -41,3 +41,22 @@ for with_eds in (False, True):
         t = time.perf_counter() - a
         gb = n * (3 if with_eds else 1) * k * k * SH / t / 1e9
         print(f"eds={with_eds} rep {r}: {t * 1e3:.1f} ms  {n / t:.0f} squares/s  {gb:.1f} GB/s", flush=True)
+
+# check: every square's EDS and data root against the device path (HBM-resident
+# extend_dah_device of the same ODS, one square at a time for a sample)
+dev = torch.device("cuda", 0)
+s = torch.cuda.current_stream(dev).cuda_stream
+bad = 0
+for i in sorted({0, 1, n // 2, n - 1}):
+    o = h_ods[i].to(dev)
+    e = torch.empty(W * W * SH, dtype=torch.uint8, device=dev)
+    rr = torch.empty(W * 90, dtype=torch.uint8, device=dev)
+    cc = torch.empty(W * 90, dtype=torch.uint8, device=dev)
+    g = torch.empty(32, dtype=torch.uint8, device=dev)
+    ctx.extend_dah_device(o.data_ptr(), k, 1, e.data_ptr(), rr.data_ptr(), cc.data_ptr(), g.data_ptr(), None, s)
+    torch.cuda.synchronize(dev)
+    ok = torch.equal(e.cpu(), h_eds[i]) and bytes(g.cpu().numpy()) == bytes(roots[i])
+    bad += not ok
+print(f"check: {4 - bad if n > 3 else n} sampled squares match the device path (EDS bytes + data root)"
+      + ("" if bad == 0 else f"; {bad} DIFFER"), flush=True)
+sys.exit(1 if bad else 0)

@@ -27,7 +27,7 @@ STAGE = {"rfc_leaf_kernel": "data_root_leaves", "data_root_digest_kernel": "data
          "leaf_kernel": "nmt_leaves", "level_kernel": "nmt_levels", "tree_top_kernel": "nmt_tree_top",
          "data_root_kernel": "data_root", "rs8_bs_half_kernel": "rs_gf8_bs", "rs8_bs_kernel": "rs_gf8_bs",
          "rs8_job_kernel": "rs_gf8", "rs16_cw_kernel": "rs_gf16", "rs16_lds_kernel": "rs_gf16_lds",
-         "rs16_half_kernel": "rs_gf16", "subtree_kernel": "nmt_levels"}   # (fused levels of k = 256 / 512 squares)
+         "rs16_half_kernel": "rs_gf16", "rs16_bs_kernel": "rs_gf16", "subtree_kernel": "nmt_levels"}   # (fused levels of k = 256 / 512 squares)
 
 
 def short(name: str) -> str:
