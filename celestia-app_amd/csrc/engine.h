@@ -299,9 +299,6 @@ class Engine {
     // Second stream of a call: half of a batch's hash stages (enqueue_dah), or
     // the batch pipeline's RS chunks (enqueue_extend_dah, CDA_PIPELINE_CHUNK).
     hipStream_t aux_stream_ = nullptr;
-    hipStream_t rs_hi_ = nullptr;   // GF(2^16) columns + Q3 (enqueue_extend)
-    hipEvent_t rs_fork_ = nullptr, rs_join_ = nullptr;
-    bool rs16_split_ = true;        // CDA_RS16_SPLIT (A/B)
     std::vector<hipEvent_t> sync_events_;
     uint32_t pipeline_chunk_ = 0;   // squares per chunk (0 = auto)
     int hash_split_ = -1;           // CDA_HASH_SPLIT: hash the batch in this many parts on as many streams (0/1 = off, -1 = auto)

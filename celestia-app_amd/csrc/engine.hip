@@ -108,9 +108,6 @@ Engine::~Engine() {
     if (copy_out_) (void)hipStreamDestroy(copy_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
     if (aux_stream_) (void)hipStreamDestroy(aux_stream_);
-    if (rs_hi_) (void)hipStreamDestroy(rs_hi_);
-    for (hipEvent_t e : {rs_fork_, rs_join_})
-        if (e) (void)hipEventDestroy(e);
     if (rs_cu_stream_) (void)hipStreamDestroy(rs_cu_stream_);
     if (hash_cu_stream_) (void)hipStreamDestroy(hash_cu_stream_);
     for (hipStream_t q : split_streams_)
@@ -194,17 +191,6 @@ int Engine::init() {
     for (hipEvent_t* e : {pipe_in_, pipe_rs_, pipe_d2h_, pipe_comp_})
         for (uint32_t i = 0; i < kPipeSlots; i++)
             if ((rc = check(hipEventCreateWithFlags(&e[i], hipEventDisableTiming), "hipEventCreate"))) return rc;
-    // GF(2^16) squares: the column codewords and Q3 on a high-priority stream
-    // beside the row codewords (enqueue_extend)
-    {
-        int least = 0, greatest = 0;
-        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-        if ((rc = check(hipStreamCreateWithPriority(&rs_hi_, hipStreamNonBlocking, greatest), "hipStreamCreate")))
-            return rc;
-        if ((rc = check(hipEventCreateWithFlags(&rs_fork_, hipEventDisableTiming), "hipEventCreate"))) return rc;
-        if ((rc = check(hipEventCreateWithFlags(&rs_join_, hipEventDisableTiming), "hipEventCreate"))) return rc;
-        if (const char* env = getenv("CDA_RS16_SPLIT")) rs16_split_ = atoi(env) != 0;
-    }
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority).
     if (const char* env = getenv("CDA_RS_PRIORITY")) {
@@ -344,30 +330,6 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
     // d_ods == NULL: in place, the ODS is already in Q0 of d_eds
     RsJob q0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
     q0.err_init = err_init;
-    if (k >= 256 && rs16_split_) {
-        // GF(2^16): three launches instead of two.  The column codewords (Q0
-        // -> Q2) and then Q3 (Q2 -> Q3) on a high-priority stream, the row
-        // codewords (Q0 -> Q1) beside them on s: the columns' workgroups are
-        // dispatched first, and Q3's fill the slots the rows free as soon as
-        // the columns are done -- instead of Q3 waiting for the rows too and
-        // both launches ending in a partial round of workgroups
-        // (2 048 + 1 024 workgroup-halves per square on 768 slots).  One
-        // k = 512 square -10 to -20 us (profiles/r04/r04t_rs16_split_ab.txt).
-        // The stage pass times the whole RS as the Q0 stage.
-        RsJob cols = q0, rows = q0;
-        cols.n_seg = rows.n_seg = 1;
-        cols.seg[0] = q0.seg[1];
-        rows.err_init = nullptr;
-        if ((rc = check(hipEventRecord(rs_fork_, s), "hipEventRecord"))) return rc;
-        if ((rc = check(hipStreamWaitEvent(rs_hi_, rs_fork_, 0), "hipStreamWaitEvent"))) return rc;
-        if ((rc = check(launch_rs(cols, k, n, t, rs_hi_), "rs Q0 columns"))) return rc;
-        if ((rc = check(launch_rs(rows, k, n, t, s), "rs Q0 rows"))) return rc;
-        if ((rc = check(launch_rs(square_job_q3(d_eds, k), k, n, t, rs_hi_), "rs Q3"))) return rc;
-        if ((rc = check(hipEventRecord(rs_join_, rs_hi_), "hipEventRecord"))) return rc;
-        if ((rc = check(hipStreamWaitEvent(s, rs_join_, 0), "hipStreamWaitEvent"))) return rc;
-        mark_end(s);
-        return CDA_OK;
-    }
     if ((rc = check(launch_rs(q0, k, n, t, s), "rs Q0"))) return rc;
     mark_end(s);
     mark_begin(kStageRsQ3, s);
