@@ -380,11 +380,155 @@ B16_HD void xor_pairs(uint32_t* R) {   // y ^= x for the pairs (i, i + D) of 8 u
         }
     });
 }
+// Greedy shared signals (Paar-style common-subexpression extraction, at
+// compile time): all networks of one butterfly read the same 16 planes y, so
+// up to kPlanSignals derived signals s[16 + i] = s[a_i] ^ s[b_i] are chosen,
+// each time the pair whose replacement saves the most 3-input-XOR ops over
+// all the butterfly's rows (base, masked lane and wave rows), and every row
+// becomes a mask over the 16 + kPlanSignals signals.  Against the fixed pair
+// sums y[2i] ^ y[2i+1] (make_sig): 6 % fewer network ops for the same 8
+// registers (tools/bs16_cse.py, profiles/r04/bs16_network_ops.txt).
+constexpr int kPlanSignals = 8;
+struct SigPlan {
+    uint8_t a[kPlanSignals], b[kPlanSignals];
+    int n;                 // derived signals in use
+    uint32_t base[16];     // row masks over 16 + kPlanSignals signals
+    uint32_t lane[4][16];
+    uint32_t wave[2][16];
+};
+// ops of a row of t signals: x ^= sum (base / wave) or x ^= sum & m (lane)
+constexpr int plan_row_ops(uint32_t msk, bool masked) {
+    const int t = __builtin_popcount(msk);
+    if (t == 0) return 0;
+    return masked ? (t - 1 + 1) / 2 + 1 : (t + 1) / 2;
+}
+constexpr SigPlan make_plan(uint32_t c0, const uint32_t* tl, int nl, const uint32_t* tw, int nw) {
+    SigPlan P{};
+    uint32_t rows[16 * 7] = {};
+    bool msk[16 * 7] = {};
+    int nr = 0;
+    auto add = [&](uint32_t c, bool masked) {
+        const Net n = make_net(c);
+        for (int i = 0; i < 16; i++) {
+            rows[nr] = n.row[i];
+            msk[nr++] = masked;
+        }
+    };
+    add(c0, false);
+    for (int l = 0; l < nl; l++) add(tl[l], true);
+    for (int w = 0; w < nw; w++) add(tw[w], false);
+    int ns = 16;
+    for (int it = 0; it < kPlanSignals; it++) {
+        // a row holding both signals of a pair drops one term: it saves
+        // ops(t) - ops(t - 1), whichever pair it is
+        int gain[16 + kPlanSignals][16 + kPlanSignals] = {};
+        for (int r = 0; r < nr; r++) {
+            const int t = __builtin_popcount(rows[r]);
+            const int d = plan_row_ops(rows[r], msk[r]) - plan_row_ops(rows[r] & (rows[r] - 1), msk[r]);
+            if (d <= 0 || t < 2) continue;
+            for (uint32_t ra = rows[r]; ra; ra &= ra - 1) {
+                const int a = __builtin_ctz(ra);
+                for (uint32_t rb = ra & (ra - 1); rb; rb &= rb - 1) gain[a][__builtin_ctz(rb)] += d;
+            }
+        }
+        int best = 1, ba = -1, bb = -1;   // a pair must save more than its own op
+        for (int a = 0; a < ns; a++)
+            for (int b = a + 1; b < ns; b++)
+                if (gain[a][b] > best) {
+                    best = gain[a][b];
+                    ba = a;
+                    bb = b;
+                }
+        if (ba < 0) break;
+        const uint32_t pm = (1u << ba) | (1u << bb);
+        for (int r = 0; r < nr; r++)
+            if ((rows[r] & pm) == pm) rows[r] = (rows[r] & ~pm) | (1u << ns);
+        P.a[it] = (uint8_t)ba;
+        P.b[it] = (uint8_t)bb;
+        ns++;
+    }
+    P.n = ns - 16;
+    int r = 0;
+    for (int i = 0; i < 16; i++) P.base[i] = rows[r++];
+    for (int l = 0; l < nl; l++)
+        for (int i = 0; i < 16; i++) P.lane[l][i] = rows[r++];
+    for (int w = 0; w < nw; w++)
+        for (int i = 0; i < 16; i++) P.wave[w][i] = rows[r++];
+    return P;
+}
+template <int LOGK, bool INV, int b, int NL, int LB, int NWB, int WB>
+constexpr SigPlan layer_plan(uint32_t c0) {
+    uint32_t tl[4] = {}, tw[2] = {};
+    for (int l = 0; l < NL; l++) tl[l] = tbasis(b, LB + l);
+    for (int w = 0; w < NWB; w++) tw[w] = tbasis(b, WB + w);
+    return make_plan(c0, tl, NL, tw, NWB);
+}
+// x ^= rows of plan P over the signals S (xor_fold / xor_sel take 32-bit masks)
+template <uint32_t MSK>
+B16_HD void plan_row(uint32_t& x, const uint32_t* S) {
+    if constexpr (MSK != 0) x = xor_fold<MSK>(x, S);
+}
+template <uint32_t MSK>
+B16_HD void plan_row_masked(uint32_t& x, const uint32_t* S, uint32_t m) {
+    if constexpr (MSK != 0) x = xor_and(x, xor_sel<MSK>(S), m);
+}
+
 // One layer over the 8 units: unit distance D, shard bit b, the unit index
 // holding shard bits from SH up (group bits of unit i: (i & ~(2D-1)) << SH),
 // NL masked lane terms (shard bits LB..), NWB uniform wave terms (bits WB..).
-// Per butterfly the pair signals of y are formed once and every term reads
+// Per butterfly the shared signals of y are formed once and every term reads
 // them; the wave terms are uniform branches.
+#ifndef CDA_BS16_PAIR_SIGNALS
+template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB>
+B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
+    sfor<0, 8, 1>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        if constexpr ((i & D) == 0) {
+            uint32_t* x = R + 16 * i;
+            uint32_t* y = R + 16 * (i + D);
+            if constexpr (INV) {
+#pragma unroll
+                for (int p = 0; p < 16; p++) y[p] ^= x[p];
+            }
+            constexpr uint32_t C0 = skew_part<INV, LOGK>(b, (uint32_t)(i & ~(2 * D - 1)) << SH);
+            constexpr SigPlan P = layer_plan<LOGK, INV, b, NL, LB, NWB, WB>(C0);
+            uint32_t S[16 + kPlanSignals];
+#pragma unroll
+            for (int p = 0; p < 16; p++) S[p] = y[p];
+            sfor<0, P.n, 1>([&](auto ss) {
+                constexpr int s = decltype(ss)::value;
+                S[16 + s] = S[P.a[s]] ^ S[P.b[s]];
+            });
+            sfor<0, 16, 1>([&](auto rr) {
+                constexpr int r = decltype(rr)::value;
+                plan_row<P.base[r]>(x[r], S);
+            });
+            sfor<0, NL, 1>([&](auto ll) {
+                constexpr int l = decltype(ll)::value;
+                sfor<0, 16, 1>([&](auto rr) {
+                    constexpr int r = decltype(rr)::value;
+                    plan_row_masked<P.lane[l][r]>(x[r], S, m[l]);
+                });
+            });
+            sfor<0, NWB, 1>([&](auto ww) {
+                constexpr int w = decltype(ww)::value;
+                if (u & (1u << w)) {
+                    sfor<0, 16, 1>([&](auto rr) {
+                        constexpr int r = decltype(rr)::value;
+                        plan_row<P.wave[w][r]>(x[r], S);
+                    });
+                }
+            });
+            if constexpr (!INV) {
+#pragma unroll
+                for (int p = 0; p < 16; p++) y[p] ^= x[p];
+            }
+            fence<16>(x);
+            fence<16>(y);
+        }
+    });
+}
+#else
 template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB>
 B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
     sfor<0, 8, 1>([&](auto ii) {
@@ -417,6 +561,7 @@ B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
         }
     });
 }
+#endif
 // LOW layer b (0..2): unit = shard bits 0..2, lane bits 3..6 (m[0..3]), wave bits 7..
 template <int LOGK, bool INV, int b>
 B16_HD void low_layer(uint32_t* R, const uint32_t* m, uint32_t u) {
