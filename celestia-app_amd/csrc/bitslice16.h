@@ -393,8 +393,11 @@ B16_HD void xor_pairs(uint32_t* R) {   // y ^= x for the pairs (i, i + D) of 8 u
 #define CDA_BS16_PLAN_SIGNALS 12
 #endif
 constexpr int kPlanSignals = CDA_BS16_PLAN_SIGNALS;
+#ifndef CDA_BS16_PLAN_TRIPLES
+#define CDA_BS16_PLAN_TRIPLES 1
+#endif
 struct SigPlan {
-    uint8_t a[kPlanSignals], b[kPlanSignals];
+    uint8_t a[kPlanSignals], b[kPlanSignals], c[kPlanSignals];   // c = 0xFF: a pair
     int n;                 // derived signals in use
     uint32_t base[16];     // row masks over 16 + kPlanSignals signals
     uint32_t lane[4][16];
@@ -422,33 +425,54 @@ constexpr SigPlan make_plan(uint32_t c0, const uint32_t* tl, int nl, const uint3
     for (int l = 0; l < nl; l++) add(tl[l], true);
     for (int w = 0; w < nw; w++) add(tw[w], false);
     int ns = 16;
+    constexpr int N = 16 + kPlanSignals;
+    int gain3[CDA_BS16_PLAN_TRIPLES ? N * N * N : 1] = {};
     for (int it = 0; it < kPlanSignals; it++) {
-        // a row holding both signals of a pair drops one term: it saves
-        // ops(t) - ops(t - 1), whichever pair it is
-        int gain[16 + kPlanSignals][16 + kPlanSignals] = {};
+        // a row holding every signal of a pair (triple) drops one (two)
+        // terms: it saves ops(t) - ops(t - 1) (ops(t) - ops(t - 2)),
+        // whichever set it is; the best set must save more than its own op
+        int gain2[N][N] = {};
+        int best = 1, ba = -1, bb = -1, bc = -1;
         for (int r = 0; r < nr; r++) {
-            const int t = __builtin_popcount(rows[r]);
-            const int d = plan_row_ops(rows[r], msk[r]) - plan_row_ops(rows[r] & (rows[r] - 1), msk[r]);
-            if (d <= 0 || t < 2) continue;
-            for (uint32_t ra = rows[r]; ra; ra &= ra - 1) {
+            const uint32_t row = rows[r];
+            const int t = __builtin_popcount(row);
+            if (t < 2) continue;
+            const uint32_t r1 = row & (row - 1), r2 = r1 & (r1 - 1);   // one / two terms fewer
+            const int d2 = plan_row_ops(row, msk[r]) - plan_row_ops(r1, msk[r]);
+            const int d3 = t >= 3 ? plan_row_ops(row, msk[r]) - plan_row_ops(r2, msk[r]) : 0;
+            for (uint32_t ra = row; ra; ra &= ra - 1) {
                 const int a = __builtin_ctz(ra);
-                for (uint32_t rb = ra & (ra - 1); rb; rb &= rb - 1) gain[a][__builtin_ctz(rb)] += d;
+                for (uint32_t rb = ra & (ra - 1); rb; rb &= rb - 1) {
+                    const int b = __builtin_ctz(rb);
+                    if (d2 > 0 && (gain2[a][b] += d2) > best) {
+                        best = gain2[a][b];
+                        ba = a, bb = b, bc = -1;
+                    }
+                    if (CDA_BS16_PLAN_TRIPLES && d3 > 0)
+                        for (uint32_t rc = rb & (rb - 1); rc; rc &= rc - 1) {
+                            const int c = __builtin_ctz(rc);
+                            int& g = gain3[(a * N + b) * N + c];
+                            if ((g += d3) > best) {
+                                best = g;
+                                ba = a, bb = b, bc = c;
+                            }
+                        }
+                }
             }
         }
-        int best = 1, ba = -1, bb = -1;   // a pair must save more than its own op
-        for (int a = 0; a < ns; a++)
-            for (int b = a + 1; b < ns; b++)
-                if (gain[a][b] > best) {
-                    best = gain[a][b];
-                    ba = a;
-                    bb = b;
-                }
+        if (CDA_BS16_PLAN_TRIPLES)
+            for (int r = 0; r < nr; r++)   // reset the entries this round touched
+                for (uint32_t ra = rows[r]; ra; ra &= ra - 1)
+                    for (uint32_t rb = ra & (ra - 1); rb; rb &= rb - 1)
+                        for (uint32_t rc = rb & (rb - 1); rc; rc &= rc - 1)
+                            gain3[(__builtin_ctz(ra) * N + __builtin_ctz(rb)) * N + __builtin_ctz(rc)] = 0;
         if (ba < 0) break;
-        const uint32_t pm = (1u << ba) | (1u << bb);
+        const uint32_t pm = (1u << ba) | (1u << bb) | (bc >= 0 ? 1u << bc : 0u);
         for (int r = 0; r < nr; r++)
             if ((rows[r] & pm) == pm) rows[r] = (rows[r] & ~pm) | (1u << ns);
         P.a[it] = (uint8_t)ba;
         P.b[it] = (uint8_t)bb;
+        P.c[it] = bc >= 0 ? (uint8_t)bc : (uint8_t)0xFF;
         ns++;
     }
     P.n = ns - 16;
@@ -501,7 +525,10 @@ B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
             for (int p = 0; p < 16; p++) S[p] = y[p];
             sfor<0, P.n, 1>([&](auto ss) {
                 constexpr int s = decltype(ss)::value;
-                S[16 + s] = S[P.a[s]] ^ S[P.b[s]];
+                if constexpr (P.c[s] == 0xFF)
+                    S[16 + s] = S[P.a[s]] ^ S[P.b[s]];
+                else
+                    S[16 + s] = xor3(S[P.a[s]], S[P.b[s]], S[P.c[s]]);
             });
             sfor<0, 16, 1>([&](auto rr) {
                 constexpr int r = decltype(rr)::value;
