@@ -388,9 +388,10 @@ B16_HD void xor_pairs(uint32_t* R) {   // y ^= x for the pairs (i, i + D) of 8 u
 // becomes a mask over the 16 + kPlanSignals signals.  Against the fixed pair
 // sums y[2i] ^ y[2i+1] (make_sig): 6 % fewer network ops for the same 8
 // registers, 11 % with 12 (tools/bs16_cse.py, profiles/r04/bs16_network_ops.txt);
-// 12 measured best on the GPU (8 / 12 / 16: profiles/r04/r04z_signal_budget_ab.txt).
+// with triples 16 measured best (profiles/r04/r04z_signal_budget_ab.txt,
+// r04zb_triple_budget_ab.txt).
 #ifndef CDA_BS16_PLAN_SIGNALS
-#define CDA_BS16_PLAN_SIGNALS 12
+#define CDA_BS16_PLAN_SIGNALS 16
 #endif
 constexpr int kPlanSignals = CDA_BS16_PLAN_SIGNALS;
 #ifndef CDA_BS16_PLAN_TRIPLES
