@@ -394,6 +394,7 @@ B16_HD void xor_pairs(uint32_t* R) {   // y ^= x for the pairs (i, i + D) of 8 u
 #define CDA_BS16_PLAN_SIGNALS 16
 #endif
 constexpr int kPlanSignals = CDA_BS16_PLAN_SIGNALS;
+static_assert(kPlanSignals >= 0 && kPlanSignals <= 16, "rows are 32-bit masks over 16 planes + the derived signals");
 #ifndef CDA_BS16_PLAN_TRIPLES
 #define CDA_BS16_PLAN_TRIPLES 1
 #endif
