@@ -210,7 +210,9 @@ B16_HD uint32_t bitsel(uint32_t a, uint32_t b, uint32_t m) {
 // acc XOR the signals y[j] for the set bits j of MSK, as 3-input XORs.
 template <uint32_t MSK, int J = 0>
 B16_HD uint32_t xor_fold(uint32_t acc, const uint32_t* y) {
-    if constexpr (J >= 32 || (MSK >> J) == 0) {
+    if constexpr (J >= 32) {
+        return acc;
+    } else if constexpr ((MSK >> J) == 0) {
         return acc;
     } else if constexpr (((MSK >> J) & 1) == 0) {
         return xor_fold<MSK, J + 1>(acc, y);
