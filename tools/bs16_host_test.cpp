@@ -1,6 +1,6 @@
 // Host check of the constexpr GF(2^16) Leopard arithmetic (celestia-app_amd/csrc/bitslice16.h)
 // against the table build leo_build<16> (leopard_tables.h): field products, the
-// whole skew vector, the networks, and the block <-> planes transpose.
+// whole skew vector, the networks, the signal plans (make_plan) and the block <-> planes transpose.
 // Build: g++ -O2 -std=c++20 -I celestia-app_amd/csrc tools/bs16_host_test.cpp -o /tmp/bs16_host_test
 #include <cstdio>
 #include <cstdlib>
@@ -207,6 +207,45 @@ int main() {
             if (bs16::skew_part<true, 8>(b, g) != bs16::skew_value(255 + g + d) && bad++ < 30)
                 printf("ifft k256 skew_part b %d g %u\n", b, g);
         }
+    // signal plans (make_plan): every derived signal reads only earlier
+    // signals, and each planned row, expanded back over the 16 planes, is the
+    // network row it replaces (base, masked lane and wave matrices)
+    int plan_sigs = 0;
+    for (int t = 0; t < 256; t++) {
+        uint32_t tl[4], tw[2];
+        for (auto& v : tl) v = bs16::skew_value(rnd() % 1023);
+        for (auto& v : tw) v = bs16::skew_value(rnd() % 1023);
+        const uint32_t c0 = bs16::skew_value(rnd() % 1023);
+        const int nl = t % 5, nw = (t / 5) % 3;
+        const bs16::SigPlan P = bs16::make_plan(c0, tl, nl, tw, nw);
+        plan_sigs += P.n;
+        uint32_t sig[48];   // signal -> mask over the 16 planes
+        for (int i = 0; i < 16; i++) sig[i] = 1u << i;
+        for (int s = 0; s < P.n; s++) {
+            const int id = 16 + s;
+            if (P.a[s] >= id || P.b[s] >= id || (P.c[s] != 0xFF && P.c[s] >= id)) {
+                if (bad++ < 40) printf("plan signal %d reads a later signal\n", id);
+                sig[id] = 0;
+                continue;
+            }
+            sig[id] = sig[P.a[s]] ^ sig[P.b[s]] ^ (P.c[s] != 0xFF ? sig[P.c[s]] : 0u);
+        }
+        auto expand = [&](uint32_t row) {
+            uint32_t m = 0;
+            for (; row; row &= row - 1) m ^= sig[__builtin_ctz(row)];
+            return m;
+        };
+        auto check = [&](const char* what, uint32_t c, const uint32_t* rows) {
+            const bs16::Net n = bs16::make_net(c);
+            for (int i = 0; i < 16; i++)
+                if (expand(rows[i]) != n.row[i] && bad++ < 40)
+                    printf("plan %s row %d c=%04x: %04x want %04x\n", what, i, c, expand(rows[i]), n.row[i]);
+        };
+        check("base", c0, P.base);
+        for (int l = 0; l < nl; l++) check("lane", tl[l], P.lane[l]);
+        for (int w = 0; w < nw; w++) check("wave", tw[w], P.wave[w]);
+    }
+    printf("signal plans: 256 checked, %.1f derived signals each\n", plan_sigs / 256.0);
     bad += check_encode<9>(*F);
     bad += check_encode<8>(*F);
     printf("%s (%d mismatches)\n", bad ? "FAIL" : "OK", bad);
