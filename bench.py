@@ -263,7 +263,16 @@ def host_pipeline_rates(ctx, k: int, d_ods, d_eds, idx, reps: int = 3) -> dict:
         h_eds.view(-1)[:par].copy_(d_eds.view(-1)[:par], non_blocking=True)
         torch.cuda.synchronize(dev)
 
-    t_h2d, t_d2h = med(h2d), med(d2h)
+    s_up, s_down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def both():   # the pipeline's mix: ODS up and parity down at once, on two streams
+        with torch.cuda.stream(s_up):
+            d_ods.view(n, -1).copy_(h_ods, non_blocking=True)
+        with torch.cuda.stream(s_down):
+            h_eds.view(-1)[:par].copy_(d_eds.view(-1)[:par], non_blocking=True)
+        torch.cuda.synchronize(dev)
+
+    t_h2d, t_d2h, t_both = med(h2d), med(d2h), med(both)
     t_roots = med(lambda: run(False))
     t_eds = med(lambda: run(True))
     g = golden_config4()
@@ -287,12 +296,14 @@ def host_pipeline_rates(ctx, k: int, d_ods, d_eds, idx, reps: int = 3) -> dict:
             "h2d_line_gb_per_s": h2d_line, "roots_only_frac_of_h2d_line": roots_gbs / h2d_line,
             "eds_to_host_squares_per_s": n / t_eds, "eds_d2h_gb_per_s": eds_gbs,
             "d2h_line_gb_per_s": d2h_line, "eds_frac_of_d2h_line": eds_gbs / d2h_line,
+            "bidir_line_squares_per_s": n / t_both, "eds_frac_of_bidir_line": t_both / t_eds,
             "parity": {"data_roots_checked": checked, "data_roots_matched": matched,
                        "eds_digests_checked": eds_checked, "eds_digests_matched": eds_matched},
             "note": "one cda_extend_dah_batch call over the rank's squares from page-locked host buffers "
                     "(torch pin_memory): ODS up, roots (and with the EDS: the three parity quadrants) down; "
                     "the library pipelines 32-square chunks over three streams; line rates = plain pinned "
-                    "copies of the same bytes in the same run, one direction at a time"}
+                    "copies of the same bytes in the same run, one direction at a time; bidir line = both copies at once "
+                    "on two streams (the pipeline's own mix of ODS up and parity down)"}
 
 
 def cpu_model() -> str:

@@ -17,6 +17,8 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "../../include/cda.h"
 #include "leopard_tables.h"
 #include "sha256_dev.h"
@@ -869,11 +871,33 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
         return v ? v : 1u;
     }();
     const unsigned nt = (unsigned)std::min<size_t>(cap, std::max<size_t>(1, rows * row / (2u << 20)));
+    // streaming stores (CDA_HOST_NT, default on): the EDS rows are not read
+    // back here, so skip the read-for-ownership of every destination line
+    static const bool nt_stores = [] {
+        const char* e = getenv("CDA_HOST_NT");
+        return e ? atoi(e) != 0 : true;
+    }();
     auto part = [&](unsigned t) {
         for (size_t i = rows * t / nt; i < rows * (t + 1) / nt; i++) {
             const size_t sq = i / k, r = i % k;
-            memcpy(eds + (sq * W * W + r * W) * kShare, ods + i * row, row);
+            uint8_t* dst = eds + (sq * W * W + r * W) * kShare;
+            const uint8_t* src = ods + i * row;
+            if (!nt_stores || ((uintptr_t)dst | (uintptr_t)src) & 15) {
+                memcpy(dst, src, row);
+                continue;
+            }
+            for (size_t o = 0; o < row; o += 64) {   // rows are whole shares (512 B)
+                const __m128i a = _mm_load_si128((const __m128i*)(src + o)),
+                              b = _mm_load_si128((const __m128i*)(src + o + 16)),
+                              c = _mm_load_si128((const __m128i*)(src + o + 32)),
+                              d = _mm_load_si128((const __m128i*)(src + o + 48));
+                _mm_stream_si128((__m128i*)(dst + o), a);
+                _mm_stream_si128((__m128i*)(dst + o + 16), b);
+                _mm_stream_si128((__m128i*)(dst + o + 32), c);
+                _mm_stream_si128((__m128i*)(dst + o + 48), d);
+            }
         }
+        _mm_sfence();
     };
     std::vector<std::thread> th;
     unsigned started = 1;   // parts [0, started) have a thread (part 0: the caller)
