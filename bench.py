@@ -342,7 +342,7 @@ def stage_report(st: dict, k: int, batch: int, inplace: bool = False, steps: int
         elif name in ("rs_q0", "rs_q3"):
             # rs_q0: read ODS, write Q0|Q1|Q2 (4 k^2 shares); rs_q3: read Q2, write Q3 (2 k^2 shares)
             # (in place there is no Q0 copy: read Q0, write Q1|Q2 = 3 k^2 shares)
-            # (k >= 256, one ticketed launch for Q0 and Q3: no separate Q3 stage, rs_q0 is the whole RS)
+            # (no separate Q3 stage recorded: rs_q0 is the whole RS)
             whole = name == "rs_q0" and st.get("rs_q3", (0.0, 0))[1] == 0
             byt = ((3 if inplace else 4) + (2 if whole else 0) if name == "rs_q0" else 2) * k * k * SHARE * batch
             rec.update(bound="hbm", achieved=byt / (avg * 1e-3) / 1e9, peak=PEAK_HBM_GBS, unit="GB/s")

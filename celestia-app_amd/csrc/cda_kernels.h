@@ -51,12 +51,6 @@ struct Gf16Dev {
 hipError_t launch_rs(const RsJob& job, uint32_t k, uint32_t n_squares, const Gf16Dev& gf16, hipStream_t stream);
 // Bitsliced GF(2^16) encode of every codeword of `job` (k = 256 or 512).
 hipError_t launch_rs16_bs(const RsJob& job, uint32_t k, uint32_t n_squares, hipStream_t stream);
-// k = 256 / 512: the whole extension (Q0 rows + columns, then Q3) of n squares
-// as ONE ticketed launch (rs_gf16_bs.hip); ctr = two 128-byte counter lines
-// (zeroed by a memset the call enqueues ahead of the launch), one set per
-// launch in flight.
-hipError_t launch_rs16_bs_square(const RsJob& q0, const RsJob& q3, uint32_t* ctr, uint32_t k, uint32_t n_squares,
-                                 hipStream_t stream);
 // rsmt2d Codec.Encode of n_code contiguous codewords of k shards x len bytes.
 hipError_t launch_rs8_flat(const uint8_t* data, uint8_t* parity, uint32_t k, uint32_t len, uint32_t n_code,
                            hipStream_t stream);

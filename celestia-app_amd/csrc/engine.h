@@ -327,12 +327,6 @@ class Engine {
     std::mutex mu_;
     std::string err_;
     DevBuf gf16_log_, gf16_exp_, gf16_skew_;
-    // GF(2^16) one-launch extension (launch_rs16_bs_square): kRsTicketSlots
-    // sets of two 128-byte counter lines, one per launch in flight
-    static constexpr uint32_t kRsTicketSlots = 16, kRsTicketWords = 64;
-    DevBuf rs_tickets_;
-    uint32_t rs_ticket_seq_ = 0;
-    bool rs_ticket_ = false;  // CDA_RS16_TICKET=1: Q0 and Q3 in one ticketed launch (measured slower: off)
     Gf16Dev gf16(uint32_t k) const;
     DevBuf leaf_, lvl_, root_slots_, dig_, err_buf_, dev_err_;
     DevBuf h_ods_, h_eds_, h_rows_, h_cols_, h_roots_;   // device staging for host-buffer calls

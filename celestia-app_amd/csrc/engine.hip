@@ -213,9 +213,6 @@ int Engine::init() {
     if (const char* env = getenv("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
-    if (const char* env = getenv("CDA_RS16_TICKET")) rs_ticket_ = atoi(env) != 0;
-    if ((rc = check(rs_tickets_.ensure(kRsTicketSlots * kRsTicketWords * 4), "hipMalloc"))) return rc;
-    if ((rc = check(hipMemset(rs_tickets_.ptr, 0, kRsTicketSlots * kRsTicketWords * 4), "hipMemset"))) return rc;
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -335,12 +332,6 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
     // d_ods == NULL: in place, the ODS is already in Q0 of d_eds
     RsJob q0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
     q0.err_init = err_init;
-    if (rs_ticket_ && (k == 256 || k == 512)) {   // Q0 and Q3 in one ticketed launch (rs_gf16_bs.hip)
-        uint32_t* ctr = rs_tickets_.as<uint32_t>() + (rs_ticket_seq_++ % kRsTicketSlots) * kRsTicketWords;
-        if ((rc = check(launch_rs16_bs_square(q0, square_job_q3(d_eds, k), ctr, k, n, s), "rs Q0+Q3"))) return rc;
-        mark_end(s);
-        return CDA_OK;
-    }
     if ((rc = check(launch_rs(q0, k, n, t, s), "rs Q0"))) return rc;
     mark_end(s);
     mark_begin(kStageRsQ3, s);

@@ -28,8 +28,6 @@
 // LOW's constants also depend on the lane (bits 3..6) and the wave (bits 7..),
 // M1's on the lane (bit 6) and the wave: the skew is linear in the group
 // position, so those enter as masked and uniform-branch terms (layer8).
-#include <algorithm>
-
 #include "bitslice16.h"
 #include "cda_kernels.h"
 
@@ -65,21 +63,21 @@ __device__ __forceinline__ void lds_ld(const u32x4* X, uint32_t idx, uint32_t* r
     r[3] = v.w;
 }
 
-// One half-codeword (4 of the 8 blocks of every shard): codeword c of
-// segment g, reading src and writing E (one square's bases).
-struct NoHook {
-    __device__ void operator()() const {}
-};
-// after_loads(): called once the codeword's loads are issued (the ticket
-// kernel stores its prefetched next ticket there)
-template <int LOGK, typename AfterLoads = NoHook>
-__device__ __forceinline__ void bs_encode_half(const uint8_t* src, uint8_t* E, const RsSeg& g, uint32_t c,
-                                               uint32_t half, u32x4* X, bool write_through = false,
-                                               AfterLoads after_loads = {}) {
+template <int LOGK>
+__global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd))) void rs16_bs_kernel(
+    const RsJob job) {
     constexpr int NW = 1 << (LOGK - 7);    // waves per workgroup
     constexpr int K = 1 << LOGK;
+    rs_err_init(job);
+    extern __shared__ u32x4 X[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, b4 = lane & 3, jl = lane >> 2;
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t cw = blockIdx.x >> 1, half = blockIdx.x & 1;
+    const bool s1 = job.n_seg > 1 && cw >= job.seg[0].n_cw;
+    const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
+    const uint32_t c = s1 ? cw - job.seg[0].n_cw : cw;
+    const uint8_t* src = job.src + (size_t)blockIdx.y * job.src_sq;
+    uint8_t* E = job.dst + (size_t)blockIdx.y * job.dst_sq;
     // LOW layout: unit u of lane (b4, jl) of wave w is shard w << 7 | jl << 3 | u,
     // block 4 half + b4: uniform part (w, u) in SGPRs + a per-lane offset
     const uint32_t blk_off = 64 * (4 * half + b4);
@@ -102,7 +100,6 @@ __device__ __forceinline__ void bs_encode_half(const uint8_t* src, uint8_t* E, c
             R[16 * u + 4 * q + 3] = v.w;
         }
     });
-    after_loads();
     if (g.cpy_off != kNoCopy) {   // the ODS copy into Q0 (packed entry)
         const uint32_t c0 = g.cpy_off + c * g.cpy_cw + (w << 7) * g.cpy_sh, lc = blk_off + 8 * jl * g.cpy_sh;
         bs16::sfor<0, 8, 1>([&](auto uu) {
@@ -186,136 +183,16 @@ __device__ __forceinline__ void bs_encode_half(const uint8_t* src, uint8_t* E, c
     x12(true);
     bs16::phase_low_fft<LOGK>(R, m, w);
     // ---- planes -> bytes, store parity -----------------------------------------
-    // write_through (uniform): sc1 stores, the parity another workgroup of
-    // the launch reads (rs16_bs_ticket_kernel); s_nop 1 after each: the
-    // compiler does not see the store's data registers in use
     bs16::sfor<0, 8, 1>([&](auto uu) {
         constexpr int u = decltype(uu)::value;
         bs16::block_planes(R + 16 * u);
         uint32_t o = d0 + u * g.dst_sh;
         asm volatile("" : "+s"(o));
         u32x4* p = reinterpret_cast<u32x4*>(E + o + ld);
-        if (write_through) {
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1"
-                             :
-                             : "v"(p + q), "v"(u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2],
-                                                    R[16 * u + 4 * q + 3]})
-                             : "memory");
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                p[q] = u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2], R[16 * u + 4 * q + 3]};
-        }
+        for (int q = 0; q < 4; q++)
+            p[q] = u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2], R[16 * u + 4 * q + 3]};
     });
-}
-
-template <int LOGK>
-__global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd))) void rs16_bs_kernel(
-    const RsJob job) {
-    rs_err_init(job);
-    extern __shared__ u32x4 X[];
-    const uint32_t cw = blockIdx.x >> 1, half = blockIdx.x & 1;
-    const bool s1 = job.n_seg > 1 && cw >= job.seg[0].n_cw;
-    const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
-    const uint32_t c = s1 ? cw - job.seg[0].n_cw : cw;
-    bs_encode_half<LOGK>(job.src + (size_t)blockIdx.y * job.src_sq, job.dst + (size_t)blockIdx.y * job.dst_sq, g, c,
-                         half, X);
-}
-
-// The whole extension of n squares in ONE launch (Q0 columns, Q0 rows, Q3):
-// every workgroup draws a ticket; tickets [0, P) are the column
-// half-codewords (Q0 -> Q2), [P, 2P) the rows (Q0 -> Q1), [2P, 3P) Q3 (Q2
-// rows -> Q3), P = n * 2k.  A Q3 workgroup needs the columns of its square
-// done; it polls the column counter, which every column workgroup bumps after
-// publishing its parity (write-through sc1 stores drained by every wave,
-// barrier, one lane's relaxed agent add: no L2 write-back), and then acquires
-// (one lane's agent acquire, drain, barrier) before its plain loads (the
-// hand-off recipe of the MI355X guide, inter-workgroup visibility; a release
-// fence per column workgroup instead measured 15-30 % slower).  No
-// deadlock whatever the dispatch order: a workgroup holding a Q3 ticket waits
-// only for workgroups that drew earlier tickets, which never wait.  The one
-// launch has no Q0 -> Q3 boundary: 3P items fill ceil(3P / resident) rounds
-// instead of ceil(2P / resident) + ceil(P / resident).  A persistent grid (the
-// resident workgroups), each drawing its next ticket while it encodes; the two
-// counters (128-byte lines) are zeroed by a memset ahead of the launch.
-typedef __attribute__((address_space(1))) uint32_t gu32;
-constexpr uint32_t kTicketLine = 32;   // u32 words per 128-byte line
-template <int LOGK>
-__global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_eu(kWavesPerSimd))) void
-rs16_bs_ticket_kernel(const RsJob job, const RsSeg q3, uint32_t* ctr_p, uint32_t n_sq) {
-    extern __shared__ u32x4 X[];
-    __shared__ uint32_t s_ticket[2];   // the next ticket, by item parity
-    gu32* ctr = (gu32*)ctr_p;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = 2u << LOGK, P = n_sq * per;   // half-codewords per square and phase; per phase
-    if (tid == 0) s_ticket[0] = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    uint32_t t = __builtin_amdgcn_readfirstlane(s_ticket[0]);
-    for (uint32_t it = 1; t < 3 * P; it ^= 1) {
-        // the next ticket, drawn now and stored once the item's loads are
-        // issued: its latency hides under them.  Always a later ticket than t,
-        // so a waiting Q3 item never holds back a column ticket (no deadlock).
-        // Slot it is written in this item and read at its end; the other slot
-        // was read by every wave before this item's first barrier.
-        uint32_t next = 0;
-        if (tid == 0) next = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t phase = t / P, r = t - phase * P, y = r / per, x = r - y * per;
-        const bool q3_item = phase == 2;
-        if (q3_item) {   // Q3: wait for every column of the launch, then acquire
-            if (tid == 0) {
-                for (uint32_t i = 0;
-                     __hip_atomic_load(ctr + kTicketLine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < P;) {
-                    __builtin_amdgcn_s_sleep(8);
-                    if (++i == (1u << 22)) break;   // bounded (~1 s): a wrong count ends in wrong parity, not a hang
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-        } else if (phase == 0 && x == 0 && tid == 0 && job.err_init) {
-            job.err_init[y] = 0xFFFFFFFFu;
-        }
-        uint8_t* E = job.dst + (size_t)y * job.dst_sq;
-        // one call site: the encoder body is instantiated once
-        bs_encode_half<LOGK>(q3_item ? E : job.src + (size_t)y * job.src_sq, E,
-                             q3_item ? q3 : phase == 0 ? job.seg[1] : job.seg[0], x >> 1, x & 1, X, phase == 0,
-                             [&] {
-                                 if (tid == 0) s_ticket[it] = next;
-                             });
-        if (phase == 0) {   // publish this half-codeword's Q2 parity (sc1 stores: no release fence)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
-            __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add(ctr + kTicketLine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();   // the item's LDS readers are done (the next item's first exchange has no barrier)
-        t = __builtin_amdgcn_readfirstlane(s_ticket[it]);
-    }
-}
-
-template <int LOGK>
-hipError_t launch_ticket(const RsJob& q0, const RsSeg& q3, uint32_t* ctr, uint32_t n, hipStream_t s) {
-    static int grid = 0;   // resident workgroups: a persistent grid (fewer admitted just start later)
-    if (!grid) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs16_bs_ticket_kernel<LOGK>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs16_lds_bytes<LOGK>());
-        if (e != hipSuccess) return e;
-        int dev = 0, cus = 0, per_cu = 0;
-        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-        if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rs16_bs_ticket_kernel<LOGK>, 64 << (LOGK - 7),
-                                                              bs16_lds_bytes<LOGK>())) != hipSuccess)
-            return e;
-        grid = std::max(1, cus * std::max(1, per_cu));
-    }
-    const uint32_t items = 3 * n * (2u << LOGK);
-    // the ticket and column counters start at zero every launch
-    hipError_t e = hipMemsetAsync(ctr, 0, 2 * kTicketLine * 4, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rs16_bs_ticket_kernel<LOGK>, dim3(std::min<uint32_t>(items, (uint32_t)grid)),
-                       dim3(64 << (LOGK - 7)), bs16_lds_bytes<LOGK>(), s, q0, q3, ctr, n);
-    return hipGetLastError();
 }
 
 template <int LOGK>
@@ -337,17 +214,6 @@ hipError_t launch_bs(const RsJob& j, uint32_t n, hipStream_t s) {
 hipError_t launch_rs16_bs(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s) {
     if (k == 512) return launch_bs<9>(j, n, s);
     if (k == 256) return launch_bs<8>(j, n, s);
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_rs16_bs_square(const RsJob& q0, const RsJob& q3, uint32_t* ctr, uint32_t k, uint32_t n,
-                                 hipStream_t s) {
-    // the ticket decode assumes both Q0 segments (rows, columns) and Q3 hold k codewords
-    if (q0.n_seg != 2 || q0.seg[0].n_cw != k || q0.seg[1].n_cw != k || q3.n_seg != 1 || q3.seg[0].n_cw != k ||
-        q3.src != q0.dst || q3.dst != q0.dst || q3.dst_sq != q0.dst_sq || !ctr || n == 0)
-        return hipErrorInvalidValue;
-    if (k == 512) return launch_ticket<9>(q0, q3.seg[0], ctr, n, s);
-    if (k == 256) return launch_ticket<8>(q0, q3.seg[0], ctr, n, s);
     return hipErrorInvalidValue;
 }
 
