@@ -1110,13 +1110,17 @@ def main():
         if v16:
             lane = v16 * n16 / c16 * 64 / (rs5 * 1e-3) / 1e12
             clk = load_pmc("rs_gf16", "effective_clock_ghz") or 2.4
-            # a stream with half-rate ops (v_perm) issues one wave64
-            # instruction per ~4 cycles per SIMD: 1024 SIMDs x 64 lanes / 4 x clock
-            issue = 1024 * 64 / 4 * clk * 1e9 / 1e12
+            # The bitsliced encoder (round 4) is an all-full-rate stream (v_bitop3 /
+            # v_xor networks; tests/test_bitslice16.py asserts it): a SIMD-32
+            # issues one wave64 instruction per 2 cycles, so the ceiling is
+            # 1024 SIMDs x 64 lanes / 2 x the measured clock (the round-3
+            # half-rate v_perm model no longer applies).
+            issue = 1024 * 64 / 2 * clk * 1e9 / 1e12
             extras["k512"]["rs_roofline"]["valu"] = {
                 "achieved": lane, "peak": PEAK_VALU_TOPS, "unit": "T lane-instr/s", "frac": lane / PEAK_VALU_TOPS,
-                "half_rate_issue_ceiling": issue, "frac_of_issue_ceiling": lane / issue, "clock_ghz": clk,
-                "source": "SQ_INSTS_VALU x 64 per square (PMC summary, one-square run), clock GRBM_GUI_ACTIVE"}
+                "full_rate_issue_ceiling": issue, "frac_of_issue_ceiling": lane / issue, "clock_ghz": clk,
+                "source": "SQ_INSTS_VALU x 64 per square (PMC summary, one-square run), clock GRBM_GUI_ACTIVE; "
+                          "ceiling = 1024 x 64 / 2 x clock (full-rate issue)"}
         # the same square 2 and 4 times per submission: the latency-bound tail
         # (top NMT levels, 12-level data-root chain) is shared by the squares
         del e5

@@ -74,12 +74,22 @@ int guarded_on(cda_ctx* ctx, const hipStream_t* stream, F&& f) {
     const hipStream_t s = stream ? *stream : e.stream();
     int rc;
     try {
-        e.order_begin(s);
-        rc = f(e);
+        rc = e.order_begin(s);
+        if (rc == CDA_OK) rc = f(e);
     } catch (const std::bad_alloc&) {
         rc = e.fail(CDA_ERR_OOM, "host allocation failed");
     } catch (...) {
         rc = e.fail(CDA_ERR_DEVICE, "unexpected exception");
+    }
+    // A failed call may have returned before joining its side streams (hash
+    // split parts, RS chunks, the host pipeline's copies): wait for them here,
+    // so nothing the call queued can still read a buffer that the next call
+    // frees in stream order, or a host buffer the caller frees on return.
+    // (Push-order results are complete answers, not failures.)
+    if (rc != CDA_OK && rc != CDA_ERR_PUSH_ORDER) {
+        const std::string msg = e.last_error();
+        (void)e.drain_streams();
+        e.fail(rc, msg);   // keep the call's own error text
     }
     e.order_end(s);
     tl_err.msg = e.last_error();
@@ -453,6 +463,7 @@ int cda_square_destroy(cda_square* sq) {
     if (!sq) return CDA_OK;
     std::lock_guard<std::mutex> g(sq->ctx->eng.mutex());
     DeviceScope dev(sq->ctx->eng.device());
+    (void)sq->ctx->eng.drain();   // no queued work of the context reads the square any more
     delete sq;
     return CDA_OK;
 }

@@ -122,6 +122,8 @@ hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
 // digests and, where every workgroup holds a power-of-two group of roots,
 // inner levels over the group; *n_dig_out (<= n_items) digests per square go
 // to dig[sq][.] for launch_data_root_digests.
+// Lane-pair SHA-256 in the tree tops and the data root (CDA_TOP_PAIR=0: off).
+bool pair_sha_enabled();
 hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n_squares, uint32_t* dig,
                            uint32_t n_items, hipStream_t stream, uint32_t* n_dig_out = nullptr, bool wide = false);
 // RFC-6962 data root over n_items 96-B root slots per square (power of two).

@@ -85,7 +85,7 @@ int Engine::comm_init(int rank, int world, const uint8_t* id) {
     // the agreement round's words (split_extend_dah): preset 0 and 1, so the
     // all-reduce needs no copy that could fail before it
     int rc;
-    if ((rc = check(comm_flag_.ensure(16), "hipMalloc agreement words"))) return rc;
+    if ((rc = check(comm_flag_.ensure_fixed(16), "hipMalloc agreement words"))) return rc;
     const int32_t preset[4] = {0, 1, 0, 0};
     if ((rc = check(hipMemcpy(comm_flag_.ptr, preset, sizeof preset, hipMemcpyHostToDevice), "hipMemcpy agreement words")))
         return rc;

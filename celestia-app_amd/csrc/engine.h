@@ -61,11 +61,19 @@ hipError_t launch_share_writer(const square::Segment* segs, uint32_t n_segs, con
 // for every earlier call of the context -- and the new one comes from
 // hipMallocAsync on it, so device entry points stay enqueue-only (no device
 // synchronisation).  Outside a call (context set-up) plain hipMalloc / hipFree.
+// A pooled buffer is usable in the call stream's order only: a host-side copy
+// into it (hipMemcpy on the null stream) is not ordered after the allocation,
+// so buffers filled from the host once (tables, preset words) use
+// ensure_fixed (plain hipMalloc, never pooled).
+// release(): inside a call, stream-ordered on the call's stream; outside a
+// call (destructors) the owner first drains every stream that may still use
+// the buffer (Engine::drain), then frees.
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
     bool pooled = false;   // allocated by hipMallocAsync
     hipError_t ensure(size_t n);
+    hipError_t ensure_fixed(size_t n);
     void release();
     template <class T>
     T* as() const { return reinterpret_cast<T*>(ptr); }
@@ -120,8 +128,30 @@ class Engine {
     // call, whatever stream it ran on -- and ends with order_end(s), which
     // records that point.  The mutex orders the enqueues, the event orders the
     // GPU work, so two calls on two streams never touch the scratch at once.
-    void order_begin(hipStream_t s);
+    // order_begin returns CDA_OK, or CDA_ERR_DEVICE when the previous call's
+    // work can be neither waited for on s nor on the host.
+    int order_begin(hipStream_t s);
     void order_end(hipStream_t s);
+    // Wait on the host until every stream the context owns (stream_, the copy,
+    // hash-split, pipeline and CU-mask streams) is idle.  Called after a failed
+    // call: a call joins its side streams back to the call stream only on its
+    // success path, and an early error return would otherwise leave side-stream
+    // work that reads the scratch unordered before the next call's
+    // stream-ordered frees.  Returns the first error.
+    int drain_streams();
+    // drain_streams + the last call's end on the caller's stream (order_ev_):
+    // nothing of the context runs any more (destructors, resident squares).
+    int drain();
+    // Tests only (CDA_FAULT, read at init): an injected error at a named point
+    // after GPU work was enqueued -- "dah_part" (enqueue_dah's side part, after
+    // its leaves and levels), "pipe_chunk" (host_pipeline, after chunk 1's
+    // compute), "extend_chunk" (the RS pipeline, after chunk 0's RS).  Fires
+    // once per context, so the follow-up calls of a test run clean.
+    bool fault_at(const char* where) {
+        if (fault_.empty() || fault_ != where) return false;
+        fault_.clear();
+        return true;
+    }
     // n push-order error words of a device entry point (context scratch), or
     // NULL when the allocation fails.
     uint32_t* err_words(uint32_t n) { return dev_err_.ensure((size_t)n * 4) == hipSuccess ? dev_err_.as<uint32_t>() : nullptr; }
@@ -260,6 +290,7 @@ class Engine {
     int top_wide_ = 2;    // CDA_TOP_WIDE: levels the tree top absorbs below the lane-pair level
     int push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* host_q0_src, uint32_t k,
                          bool src_is_eds);
+    std::string fault_;   // CDA_FAULT (tests only)
 
     struct Mark {
         int stage;

@@ -51,6 +51,12 @@ hipError_t DevBuf::ensure(size_t n) {
         bytes = want;
         return hipSuccess;
     }
+    return ensure_fixed(n);
+}
+
+hipError_t DevBuf::ensure_fixed(size_t n) {
+    if (n <= bytes && ptr && !pooled) return hipSuccess;
+    const size_t want = n < 256 ? 256 : n;
     release();
     hipError_t e = hipMalloc(&ptr, want);
     if (e != hipSuccess) {
@@ -65,7 +71,10 @@ hipError_t DevBuf::ensure(size_t n) {
 
 void DevBuf::release() {
     if (ptr) {
-        if (pooled) {
+        if (pooled && tl_in_call) {
+            (void)hipFreeAsync(ptr, tl_call_stream);   // after the call's work, in stream order
+        } else if (pooled) {
+            // outside a call: the owner drained the streams that used it
             (void)hipFreeAsync(ptr, nullptr);
             (void)hipStreamSynchronize(nullptr);
         } else {
@@ -81,6 +90,11 @@ Engine::Engine(int device) : device_(device) {}
 
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
+    // every stream that may still read a buffer -- the context's own and the
+    // last caller's (order_ev_) -- is idle before anything goes back to the
+    // pool (round 4: pooled buffers were freed on the null stream, which does
+    // not order against the context's non-blocking streams)
+    (void)drain();
     for (DevBuf* b : {&gf16_log_, &gf16_exp_,
                       &gf16_skew_, &leaf_, &lvl_, &root_slots_, &dig_, &err_buf_, &dev_err_, &h_ods_, &h_eds_,
                       &h_rows_, &h_cols_, &h_roots_, &sq_plan_, &sq_txs_, &cm_plan_, &cm_tables_,
@@ -213,12 +227,13 @@ int Engine::init() {
     if (const char* env = getenv("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
+    if (const char* env = getenv("CDA_FAULT")) fault_ = env;
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
-    if ((rc = check(gf16_log_.ensure(sizeof F->log), "hipMalloc"))) return rc;
-    if ((rc = check(gf16_exp_.ensure(sizeof F->exp), "hipMalloc"))) return rc;
-    if ((rc = check(gf16_skew_.ensure(sizeof F->skew), "hipMalloc"))) return rc;
+    if ((rc = check(gf16_log_.ensure_fixed(sizeof F->log), "hipMalloc"))) return rc;
+    if ((rc = check(gf16_exp_.ensure_fixed(sizeof F->exp), "hipMalloc"))) return rc;
+    if ((rc = check(gf16_skew_.ensure_fixed(sizeof F->skew), "hipMalloc"))) return rc;
     if ((rc = check(hipMemcpy(gf16_log_.ptr, F->log, sizeof F->log, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     if ((rc = check(hipMemcpy(gf16_exp_.ptr, F->exp, sizeof F->exp, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     if ((rc = check(hipMemcpy(gf16_skew_.ptr, F->skew, sizeof F->skew, hipMemcpyHostToDevice), "hipMemcpy")))
@@ -249,7 +264,10 @@ uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n, bool* wide) const {
         if ((uint64_t)n * 2 * W * (m / 2) >= 65536) continue;
         if (m > 256) return 0;
         uint32_t t = m;
-        for (int e = 0; e < top_wide_ && 2 * t <= W && 2 * t <= 512 && 2 * t >= 8 &&
+        // the wide first level runs lane pairs above it: none without pairs
+        // (a one-thread-per-parent top holds at most 256 nodes)
+        const int widen = pair_sha_enabled() ? top_wide_ : 0;
+        for (int e = 0; e < widen && 2 * t <= W && 2 * t <= 512 && 2 * t >= 8 &&
                         2 * (uint64_t)n * 2 * W * (t / 2) <= 131072;
              e++)
             t *= 2;
@@ -259,18 +277,44 @@ uint32_t Engine::top_fuse_nodes(uint32_t W, uint32_t n, bool* wide) const {
     return 0;
 }
 
-void Engine::order_begin(hipStream_t s) {
+int Engine::order_begin(hipStream_t s) {
     tl_in_call = true;
     tl_call_stream = s;
-    if (!order_used_) return;
+    if (!order_used_) return CDA_OK;
     // the previous calls' work is complete (without a fault): nothing of it can
     // surface later, and there is nothing to order after (no wait packet ahead
     // of this call's first launch: the latency path's calls find it complete)
     if (hipEventQuery(order_ev_) == hipSuccess) {
         pending_.clear();
-        return;
+        return CDA_OK;
     }
-    (void)hipStreamWaitEvent(s, order_ev_, 0);
+    if (hipStreamWaitEvent(s, order_ev_, 0) == hipSuccess) return CDA_OK;
+    // the wait could not be enqueued: wait on the host instead (a fault of the
+    // previous work surfaces here, named by check())
+    (void)hipGetLastError();
+    return check(hipEventSynchronize(order_ev_), "hipEventSynchronize (previous call's work)");
+}
+
+int Engine::drain_streams() {
+    int first = CDA_OK;
+    auto sync = [&](hipStream_t q) {
+        if (!q) return;
+        const hipError_t e = hipStreamSynchronize(q);
+        if (e != hipSuccess && first == CDA_OK) first = check(e, "hipStreamSynchronize (drain)");
+        else if (e != hipSuccess) (void)hipGetLastError();
+    };
+    for (hipStream_t q : {stream_, copy_in_, copy_out_, aux_stream_, rs_cu_stream_, hash_cu_stream_}) sync(q);
+    for (hipStream_t q : split_streams_) sync(q);
+    return first;
+}
+
+int Engine::drain() {
+    int rc = drain_streams();
+    if (order_used_ && order_ev_) {
+        const hipError_t e = hipEventSynchronize(order_ev_);
+        if (e != hipSuccess && rc == CDA_OK) rc = check(e, "hipEventSynchronize (drain)");
+    }
+    return rc;
 }
 
 void Engine::order_end(hipStream_t s) {
@@ -573,21 +617,52 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
         // caller's stream.  Each part also finishes its own trees and data
         // roots, so one part's latency-bound data root runs under another's
         // levels.
+        // Every side part that started is joined back to s on every return
+        // path, the error returns included: a part that failed half-way may
+        // have queued leaves / levels reading the scratch, and the next call
+        // orders itself after s only.
+        int err = CDA_OK;
+        uint32_t joined_from = parts;   // side parts [joined_from, parts) recorded their end on sync_event(p)
         for (uint32_t p = parts; p-- > 0;) {
             const uint32_t i0 = p * n / parts, i1 = (p + 1) * n / parts;
             hipStream_t q = s;
             if (p) {
-                if ((rc = split_stream(p - 1, &q))) return rc;
-                if ((rc = check(hipStreamWaitEvent(q, go, 0), "hipStreamWaitEvent"))) return rc;
+                if ((rc = split_stream(p - 1, &q))) {
+                    err = rc;
+                    break;
+                }
+                if ((rc = check(hipStreamWaitEvent(q, go, 0), "hipStreamWaitEvent"))) {   // nothing queued on q
+                    err = rc;
+                    break;
+                }
             }
             Forest pp[2];
-            if ((rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q, true))) return rc;
-            if ((rc = dah_finish(k, i0, i1 - i0, stop, pp, d_roots, d_err, d_status, q))) return rc;
-            if (p && (rc = check(hipEventRecord(sync_event(p), q), "hipEventRecord"))) return rc;
+            rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q, true);
+            if (!rc) rc = dah_finish(k, i0, i1 - i0, stop, pp, d_roots, d_err, d_status, q);
+            if (!rc && p && fault_at("dah_part"))
+                rc = fail(CDA_ERR_DEVICE, "enqueue_dah: injected fault after a side part's hashing (CDA_FAULT=dah_part)");
+            if (p) {
+                if (hipEventRecord(sync_event(p), q) == hipSuccess) {
+                    joined_from = p;
+                } else {   // cannot join by event: wait for the part on the host
+                    (void)hipGetLastError();
+                    (void)hipStreamSynchronize(q);
+                    if (!rc) rc = fail(CDA_ERR_DEVICE, "hipEventRecord failed (hash split join)");
+                }
+            }
+            if (rc) {
+                err = rc;
+                break;
+            }
         }
-        for (uint32_t p = 1; p < parts; p++)
-            if ((rc = check(hipStreamWaitEvent(s, sync_event(p), 0), "hipStreamWaitEvent"))) return rc;
-        return CDA_OK;
+        for (uint32_t p = joined_from; p < parts; p++) {
+            if (hipStreamWaitEvent(s, sync_event(p), 0) == hipSuccess) continue;
+            (void)hipGetLastError();
+            hipStream_t q = nullptr;
+            if (split_stream(p - 1, &q) == CDA_OK) (void)hipStreamSynchronize(q);
+            if (!err) err = fail(CDA_ERR_DEVICE, "hipStreamWaitEvent failed (hash split join)");
+        }
+        return err;
     }
     if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s, true))) return rc;
     return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
@@ -767,7 +842,9 @@ int Engine::enqueue_extend_dah(const uint8_t* d_ods, uint32_t k, uint32_t n, uin
     for (uint32_t i = cu_split ? 1 : 0; i < n_chunks; i++) {
         const uint32_t i0 = i * c, m = (i0 + c <= n) ? c : n - i0;
         if ((rc = enqueue_extend(d_ods ? d_ods + i0 * ods_sq : nullptr, k, m, d_eds + i0 * eds_sq, rs_q)))
-            return rc;
+            return rc;   // rs_q is joined by the caller's drain (guarded_on)
+        if (fault_at("extend_chunk"))
+            return fail(CDA_ERR_DEVICE, "enqueue_extend_dah: injected fault after a chunk's RS (CDA_FAULT=extend_chunk)");
         hipEvent_t ev = sync_event(1 + i);
         if ((rc = check(hipEventRecord(ev, rs_q), "hipEventRecord"))) return rc;
     }
@@ -986,6 +1063,10 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
                               h_roots_.as<uint8_t>() + (size_t)i0 * 32, err + i0, nullptr, s, true)))
             return rc;
         if ((rc = check(hipEventRecord(pipe_comp_[slot], s), "hipEventRecord"))) return rc;
+        // (an error return leaves copies queued on copy_in_ / copy_out_: the
+        // caller's drain (guarded_on) waits for them before the call returns)
+        if (i == 1 && fault_at("pipe_chunk"))
+            return fail(CDA_ERR_DEVICE, "host_pipeline: injected fault after chunk 1 (CDA_FAULT=pipe_chunk)");
     }
     if ((rc = check(hipMemcpyAsync(rows, h_rows_.ptr, n * root_sq, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     if ((rc = check(hipMemcpyAsync(cols, h_cols_.ptr, n * root_sq, hipMemcpyDeviceToHost, s), "D2H"))) return rc;

@@ -997,7 +997,7 @@ hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
 
 // CDA_TOP_PAIR=0 (A/B knob): one thread per parent in the tree tops and the
 // data root instead of the lane-pair compression.
-static bool pair_sha_enabled() {
+bool pair_sha_enabled() {
     static const bool v = [] {
         const char* e = getenv("CDA_TOP_PAIR");
         return !(e && atoi(e) == 0);

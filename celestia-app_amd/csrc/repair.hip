@@ -297,7 +297,7 @@ int Engine::ensure_gf8_tables() {
     for (auto [buf, src, len] : {std::tuple{&gf8_log_, (const void*)F->log, sizeof F->log},
                                  std::tuple{&gf8_exp_, (const void*)F->exp, sizeof F->exp},
                                  std::tuple{&gf8_skew_, (const void*)F->skew, sizeof F->skew}}) {
-        if ((rc = check(buf->ensure(len), "hipMalloc"))) return rc;
+        if ((rc = check(buf->ensure_fixed(len), "hipMalloc"))) return rc;   // filled by a host copy below
         if ((rc = check(hipMemcpy(buf->ptr, src, len, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     }
     return CDA_OK;

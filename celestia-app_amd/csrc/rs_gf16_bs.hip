@@ -7,12 +7,12 @@
 // - 1]), on symbols b[i] | b[i + 32] << 8 of every 64-byte block.
 //
 // MI355X mapping.  TWO workgroups per codeword, each over 4 of the 8 64-byte
-// blocks of every shard (Leopard is independent per symbol position), and two
-// workgroups per CU, so one's loads, stores, exchanges and barrier waits run
-// under the other's XOR networks (k = 512: 4 waves, 256 threads, 64 KiB of
-// LDS each).  A lane holds 8 "units" -- the 16 bit-planes of the 32 symbols of
-// one block of one shard (128 VGPRs, bitslice16.h) -- so GF addition is one
-// XOR per plane and multiplying by a butterfly constant is a compile-time XOR
+// blocks of every shard (Leopard is independent per symbol position), and
+// three workgroups per CU (k = 512: 4 waves, 256 threads, 168 VGPRs and
+// 32 KiB of LDS each), so one's loads, stores, exchanges and barrier waits
+// run under the others' XOR networks.  A lane holds 8 "units" -- the 16
+// bit-planes of the 32 symbols of one block of one shard (128 VGPRs,
+// bitslice16.h) -- so GF addition is one XOR per plane and multiplying by a butterfly constant is a compile-time XOR
 // network of full-rate v_bitop3 / v_xor (about 2 SIMD cycles per
 // wave-instruction; the byte-form v_perm multiply it replaces issues at the
 // half rate and needs 3.6x the instructions: tools/bs16_probe.hip,
@@ -28,6 +28,8 @@
 // LOW's constants also depend on the lane (bits 3..6) and the wave (bits 7..),
 // M1's on the lane (bit 6) and the wave: the skew is linear in the group
 // position, so those enter as masked and uniform-branch terms (layer8).
+#include <mutex>
+
 #include "bitslice16.h"
 #include "cda_kernels.h"
 
@@ -198,13 +200,15 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
 template <int LOGK>
 hipError_t launch_bs(const RsJob& j, uint32_t n, hipStream_t s) {
     const uint32_t ncw = j.seg[0].n_cw + (j.n_seg > 1 ? j.seg[1].n_cw : 0);
-    static bool attr = false;   // function attribute, set once per instantiation
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(rs16_bs_kernel<LOGK>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs16_lds_bytes<LOGK>());
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    // function attribute, set once per instantiation (contexts on several host
+    // threads may launch at once)
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(rs16_bs_kernel<LOGK>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs16_lds_bytes<LOGK>());
+    });
+    if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(rs16_bs_kernel<LOGK>, dim3(2 * ncw, n), dim3(64 << (LOGK - 7)), bs16_lds_bytes<LOGK>(), s, j);
     return hipGetLastError();
 }

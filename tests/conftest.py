@@ -19,3 +19,21 @@ def pytest_configure(config):
 def ctx():
     import celestia_da
     return celestia_da.default_context()
+
+
+def pytest_runtest_makereport(item, call):
+    """Keep the full text of every failing GPU test (the engine's error message
+    names the stages enqueued since the context's work was last seen
+    complete), so a fault seen once is on record: gpurun_out/gpu_failures.log
+    (merged back from the GPU box; copied into profiles/ when it happens)."""
+    if call.excinfo is None or item.get_closest_marker("gpu") is None:
+        return
+    try:
+        import datetime
+        d = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "gpu_failures.log"), "a") as f:
+            f.write(f"==== {datetime.datetime.now().isoformat()} {item.nodeid} ({call.when})\n")
+            f.write(str(call.excinfo.getrepr(style="long")) + "\n")
+    except Exception:
+        pass
