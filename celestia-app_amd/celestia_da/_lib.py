@@ -37,6 +37,15 @@ CDA_ERR_COMM = -11
 CDA_SQUARE_CONSTRUCT = 0
 CDA_SQUARE_BUILD = 1
 
+# cda_split_offsets selectors (include/cda.h)
+CDA_SPLIT_SEND = 0
+CDA_SPLIT_SEND_PIECE = 1
+CDA_SPLIT_RECV_PIECE = 2
+CDA_SPLIT_BLOCK = 3
+CDA_SPLIT_GATHER_SUB = 4
+CDA_SPLIT_GATHER_COL = 5
+CDA_SPLIT_COMBINE = 6
+
 EXPORTED = (
     "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
     "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
@@ -49,7 +58,7 @@ EXPORTED = (
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
     "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
     "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_comm_abort", "cda_extend_dah_split", "cda_split_rows_send",
-    "cda_extend_dah_multi",
+    "cda_extend_dah_multi", "cda_split_layout", "cda_split_offsets",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -79,6 +88,14 @@ class UnrepairableError(CdaError):
 
 class SquareError(CdaError):
     """go-square square.Construct / Build error."""
+
+
+class SplitLayoutT(C.Structure):
+    """cda_split_layout_t (include/cda.h)."""
+    _fields_ = [(n, C.c_uint32) for n in ("k", "world", "W", "R", "C")] + \
+               [(n, C.c_uint64) for n in ("piece_bytes", "send_bytes", "col_block_bytes", "col_slots_off",
+                                          "row_sub_off", "gather_sub_off", "gather_col_off", "err_off",
+                                          "slots_bytes")]
 
 
 _lib = None
@@ -159,10 +176,36 @@ def load():
         L.cda_split_rows_send.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.cda_extend_dah_multi.argtypes = [C.POINTER(ctxp), C.c_uint32, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p,
                                            u8p, i32p]
+        L.cda_split_layout.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(SplitLayoutT)]
+        L.cda_split_offsets.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, u32p, u32p, u64p]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
         _lib = L
         return L
+
+
+def split_layout(k: int, world: int) -> dict:
+    """cda_split_layout: config 5's buffer sizes and slot offsets (host only)."""
+    out = SplitLayoutT()
+    rc = load().cda_split_layout(k, world, C.byref(out))
+    if rc != CDA_OK:
+        raise CdaError(rc, f"invalid split: k={k} world={world}")
+    return {n: getattr(out, n) for n, _ in SplitLayoutT._fields_}
+
+
+def split_offsets(k: int, world: int, what: int, a, b=None) -> np.ndarray:
+    """cda_split_offsets for arrays a, b (uint32): the split's byte offsets /
+    slot indexes computed by the library's own layout functions."""
+    a = np.ascontiguousarray(a, dtype=np.uint32)
+    bb = None if b is None else np.ascontiguousarray(b, dtype=np.uint32)
+    out = np.empty(a.size, dtype=np.uint64)
+    u32p = C.POINTER(C.c_uint32)
+    rc = load().cda_split_offsets(k, world, what, a.size, a.ctypes.data_as(u32p),
+                                  None if bb is None else bb.ctypes.data_as(u32p),
+                                  out.ctypes.data_as(C.POINTER(C.c_uint64)))
+    if rc != CDA_OK:
+        raise CdaError(rc, f"cda_split_offsets({k}, {world}, {what}) failed")
+    return out
 
 
 def ptr(a: np.ndarray | None):

@@ -10,6 +10,7 @@
 
 #include "../../include/cda.h"
 #include "engine.h"
+#include "split_layout.h"
 
 struct cda_ctx {
     cda::Engine eng;
@@ -638,6 +639,37 @@ int cda_extend_dah_split(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, void*
                                   static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
                                   static_cast<uint8_t*>(d_data_root), d_err, s);
     });
+}
+
+int cda_split_layout(uint32_t k, uint32_t world, cda_split_layout_t* out) {
+    if (!out) return CDA_ERR_INVALID;
+    const cda::SplitLayout L(k, world ? world : 1);
+    if (!world || !L.valid() || world > 2 * k) return CDA_ERR_INVALID;
+    *out = cda_split_layout_t{L.k, L.G, L.W, L.R, L.C, L.piece(), L.send_bytes(), L.col_block_bytes(),
+                              L.col_slots_off(), L.row_sub_off(), L.gather_sub_off(0), L.gather_col_off(0),
+                              L.err_off(), L.slots_bytes()};
+    return CDA_OK;
+}
+
+int cda_split_offsets(uint32_t k, uint32_t world, int what, uint32_t n, const uint32_t* a, const uint32_t* b,
+                      uint64_t* off) {
+    if (!world || !off || (n && !a)) return CDA_ERR_INVALID;
+    const cda::SplitLayout L(k, world);
+    if (!L.valid()) return CDA_ERR_INVALID;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t x = a[i], y = b ? b[i] : 0;
+        switch (what) {
+            case CDA_SPLIT_SEND: off[i] = L.send_off(x, y); break;
+            case CDA_SPLIT_SEND_PIECE: off[i] = L.send_piece_off(x); break;
+            case CDA_SPLIT_RECV_PIECE: off[i] = L.recv_piece_off(x); break;
+            case CDA_SPLIT_BLOCK: off[i] = L.block_off(x, y); break;
+            case CDA_SPLIT_GATHER_SUB: off[i] = L.gather_sub_off(x); break;
+            case CDA_SPLIT_GATHER_COL: off[i] = L.gather_col_off(x); break;
+            case CDA_SPLIT_COMBINE: off[i] = L.combine_slot(x, y); break;
+            default: return CDA_ERR_INVALID;
+        }
+    }
+    return CDA_OK;
 }
 
 int cda_extend_dah_multi(cda_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* ods, uint32_t k, uint32_t n,

@@ -25,23 +25,23 @@
 #include "../../include/cda.h"
 #include "engine.h"
 #include "sha256_dev.h"
+#include "split_layout.h"
 
 namespace cda {
 
 namespace {
 
-// [R][W] row block -> [G][R][C] send layout (dst g = columns [g*C, g*C+C)):
-// one thread per 16 bytes.
-__global__ __launch_bounds__(256) void group_rows_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                        uint32_t R, uint32_t W, uint32_t C) {
+// [R][W] row block -> [G][R][C] send layout (SplitLayout::send_off): one
+// thread per 16 bytes.
+__global__ __launch_bounds__(256) void group_rows_kernel(const uint4* __restrict__ src, uint8_t* __restrict__ dst,
+                                                        const SplitLayout L) {
     constexpr uint32_t V = kShare / 16;   // uint4 per share
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (uint64_t)R * W * V) return;
+    if (i >= (uint64_t)L.R * L.W * V) return;
     const uint32_t v = (uint32_t)(i % V);
     const uint64_t cell = i / V;
-    const uint32_t r = (uint32_t)(cell / W), col = (uint32_t)(cell % W);
-    const uint32_t g = col / C, c = col % C;
-    dst[(((uint64_t)g * R + r) * C + c) * V + v] = src[i];
+    const uint32_t r = (uint32_t)(cell / L.W), col = (uint32_t)(cell % L.W);
+    reinterpret_cast<uint4*>(dst + L.send_off(r, col))[v] = src[i];
 }
 
 // CDA_COMM_FAULT (tests only, read at every split call): make one step fail
@@ -61,14 +61,17 @@ int Engine::enqueue_split_rows_send(const uint8_t* d_rows, uint32_t k, uint32_t 
     const uint32_t W = 2 * k;
     if (parts == 0 || (parts & (parts - 1)) || parts > W || n_rows == 0)
         return fail(CDA_ERR_INVALID, "bad split: parts must be a power of two <= 2k");
-    const uint32_t C = W / parts;
     int rc;
     if (parts == 1) return enqueue_split_rows(d_rows, k, n_rows, row0, d_send, d_err, s);   // [1][R][W] = [R][W]
     if ((rc = check(split_blk_.ensure((size_t)n_rows * W * kShare), "hipMalloc row block"))) return rc;
     if ((rc = enqueue_split_rows(d_rows, k, n_rows, row0, split_blk_.as<uint8_t>(), d_err, s))) return rc;
+    // the layout of a split into `parts` column groups, with this call's row
+    // count (cda_split_rows_send callers may pass any R)
+    SplitLayout L(k, parts);
+    L.R = n_rows;
     const uint64_t n16 = (uint64_t)n_rows * W * (kShare / 16);
     hipLaunchKernelGGL(group_rows_kernel, dim3((uint32_t)((n16 + 255) / 256)), dim3(256), 0, s,
-                       split_blk_.as<uint4>(), reinterpret_cast<uint4*>(d_send), n_rows, W, C);
+                       split_blk_.as<uint4>(), d_send, L);
     return check(hipGetLastError(), "group rows");
 }
 
@@ -197,19 +200,18 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
                              uint8_t* d_col_roots, uint8_t* d_root, uint32_t* d_err, hipStream_t s) {
     if (!comm_alive()) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
     const uint32_t G = (uint32_t)world_, W = 2 * k;
-    if (k == 0 || (k & (k - 1)) || (G & (G - 1)) || k % G || k > 1024)
-        return fail(CDA_ERR_INVALID, "world size must divide k (a power of two <= 1024)");
-    const uint32_t R = k / G, C = W / G;
-    const size_t piece = (size_t)R * C * kShare;   // one rank pair's all-to-all block
-    const size_t own = (size_t)(C + W) * kSlot, all = (size_t)G * (C + W) * kSlot;
+    const SplitLayout L(k, G);   // every offset below (split_layout.h, pinned at G > 1 by a CPU replay)
+    if (!L.valid()) return fail(CDA_ERR_INVALID, "world size must divide k (a power of two <= 1024)");
+    const uint32_t R = L.R, C = L.C;
+    const size_t piece = L.piece();   // one rank pair's all-to-all block
     int rc;
     // -- scratch + agreement (only when k changes; k is the same on every rank) --
     if (comm_k_ != k) {
         int ok = 1;
         if (comm_fault("alloc")) ok = 0;
-        if (ok && G > 1 && split_send_.ensure(piece * G) != hipSuccess) ok = 0;
-        if (ok && split_col_.ensure((size_t)W * C * kShare) != hipSuccess) ok = 0;
-        if (ok && split_slots_.ensure(own + all + 64) != hipSuccess) ok = 0;
+        if (ok && G > 1 && split_send_.ensure(L.send_bytes()) != hipSuccess) ok = 0;
+        if (ok && split_col_.ensure(L.col_block_bytes()) != hipSuccess) ok = 0;
+        if (ok && split_slots_.ensure(L.slots_bytes()) != hipSuccess) ok = 0;
         // the column stage's leaf / level slots too, so no buffer grows (and
         // synchronises) once the collectives are queued
         if (ok && leaf_.ensure((size_t)W * C * kSlot) != hipSuccess) ok = 0;
@@ -237,12 +239,13 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
     uint8_t* block = d_col_block ? d_col_block : split_col_.as<uint8_t>();
     // slots: this rank's column roots [C] and row subtrees [W]; rank 0 also
     // the gathered [G][W] subtrees and [W] column roots (rank order)
-    uint8_t* col_slots = split_slots_.as<uint8_t>();
-    uint8_t* row_sub = col_slots + (size_t)C * kSlot;
-    uint8_t* g_sub = col_slots + own;                        // [G][W][96]
-    uint8_t* g_col = g_sub + (size_t)G * W * kSlot;          // [G*C = W][96]
+    uint8_t* slots = split_slots_.as<uint8_t>();
+    uint8_t* col_slots = slots + L.col_slots_off();
+    uint8_t* row_sub = slots + L.row_sub_off();
+    uint8_t* g_sub = slots + L.gather_sub_off(0);            // [G][W][96]
+    uint8_t* g_col = slots + L.gather_col_off(0);            // [G*C = W][96]
     // the push-order word: the caller's, or library scratch when it passed none
-    uint32_t* err = d_err ? d_err : reinterpret_cast<uint32_t*>(g_col + (size_t)W * kSlot);
+    uint32_t* err = d_err ? d_err : reinterpret_cast<uint32_t*>(slots + L.err_off());
     int local = CDA_OK;                                      // first local failure
     std::string local_msg;
     auto local_fail = [&](int code, const std::string& msg) {
@@ -279,9 +282,11 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
                  if (comm_fault("a2a")) return (int)ncclInternalError;
                  ncclComm_t comm = static_cast<ncclComm_t>(cv);
                  for (uint32_t h = 0; h < G; h++) {
-                     ncclResult_t q = ncclSend(split_send_.as<uint8_t>() + h * piece, piece, ncclUint8, (int)h, comm, s);
+                     ncclResult_t q = ncclSend(split_send_.as<uint8_t>() + L.send_piece_off(h), piece, ncclUint8, (int)h,
+                                               comm, s);
                      if (q != ncclSuccess) return (int)q;
-                     if ((q = ncclRecv(block + h * piece, piece, ncclUint8, (int)h, comm, s)) != ncclSuccess) return (int)q;
+                     if ((q = ncclRecv(block + L.recv_piece_off(h), piece, ncclUint8, (int)h, comm, s)) != ncclSuccess)
+                         return (int)q;
                  }
                  return (int)ncclSuccess;
              })))
@@ -302,10 +307,10 @@ int Engine::split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_b
              ncclResult_t q;
              if (rank_ == 0) {
                  for (uint32_t h = 0; h < G; h++) {
-                     if ((q = ncclRecv(g_sub + (size_t)h * W * kSlot, (size_t)W * kSlot, ncclUint8, (int)h, comm, s)) !=
+                     if ((q = ncclRecv(slots + L.gather_sub_off(h), (size_t)W * kSlot, ncclUint8, (int)h, comm, s)) !=
                          ncclSuccess)
                          return (int)q;
-                     if ((q = ncclRecv(g_col + (size_t)h * C * kSlot, (size_t)C * kSlot, ncclUint8, (int)h, comm, s)) !=
+                     if ((q = ncclRecv(slots + L.gather_col_off(h), (size_t)C * kSlot, ncclUint8, (int)h, comm, s)) !=
                          ncclSuccess)
                          return (int)q;
                  }

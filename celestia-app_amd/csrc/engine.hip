@@ -22,6 +22,7 @@
 #include "../../include/cda.h"
 #include "leopard_tables.h"
 #include "sha256_dev.h"
+#include "split_layout.h"
 
 namespace cda {
 
@@ -729,8 +730,12 @@ int Engine::enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint
         if ((rc = check(hipMemcpyAsync(rs, d_row_sub, (size_t)W * kSlot, hipMemcpyDeviceToDevice, s), "copy")))
             return rc;
     } else {
-        // row tree r: nodes (g, r) of [parts][W] -> top log2(parts) levels
-        Forest fr{d_row_sub, 0, W, 1, W, nullptr, 0, nullptr, 0, rs, 0, 0};
+        // row tree r: nodes (g, r) of the gathered [parts][W] -> top
+        // log2(parts) levels (SplitLayout::combine_slot: tree stride 1, node stride W)
+        const SplitLayout L(k, parts);
+        const uint32_t tstride = (uint32_t)(L.combine_slot(0, 1) - L.combine_slot(0, 0));
+        const uint32_t nstride = (uint32_t)(L.combine_slot(1, 0) - L.combine_slot(0, 0));
+        Forest fr{d_row_sub, 0, W, tstride, nstride, nullptr, 0, nullptr, 0, rs, 0, 0};
         const uint64_t off0[1] = {0};
         if ((rc = run_forests(&fr, 1, parts, 1, lvl_.as<uint8_t>(), leaf_.as<uint8_t>(), 0, off0, s))) return rc;
     }

@@ -240,6 +240,37 @@ int cda_extend_dah_split(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, void 
  * pieces ARE rows 0..k-1 of the receiver's column block. */
 int cda_split_rows_send(cda_ctx *ctx, const void *d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
                         uint32_t parts, void *d_send, uint32_t *d_err, void *stream);
+/* The split's buffer arithmetic (host only, no context; csrc/split_layout.h,
+ * the same functions the group-rows kernel and cda_extend_dah_split use), so a
+ * host can size its buffers and a test can replay the G > 1 exchange on the
+ * CPU.  Byte sizes / offsets: the all-to-all piece of one rank pair, the send
+ * buffer [G][R][C][512], the column block [W][C][512], and in the slot area
+ * (96-B NMT node slots) the rank's C column roots, its W row subtree nodes,
+ * (rank 0) the gathered [G][W] subtrees and [W] column roots, the push-order
+ * word.  CDA_ERR_INVALID unless k and world are powers of two, world | k. */
+typedef struct {
+    uint32_t k, world, W, R, C;
+    uint64_t piece_bytes, send_bytes, col_block_bytes;
+    uint64_t col_slots_off, row_sub_off, gather_sub_off, gather_col_off, err_off, slots_bytes;
+} cda_split_layout_t;
+int cda_split_layout(uint32_t k, uint32_t world, cda_split_layout_t *out);
+/* n offsets at once, off[i] for (a[i], b[i]) (b may be NULL when unused):
+ *   CDA_SPLIT_SEND        send-buffer byte offset of row-block cell (r = a, col = b)
+ *   CDA_SPLIT_SEND_PIECE  send-buffer byte offset of the piece for rank a
+ *   CDA_SPLIT_RECV_PIECE  column-block byte offset where rank a's piece lands
+ *   CDA_SPLIT_BLOCK       column-block byte offset of EDS row a, local column b
+ *   CDA_SPLIT_GATHER_SUB  slot-area byte offset of rank a's W row subtrees (rank 0)
+ *   CDA_SPLIT_GATHER_COL  slot-area byte offset of rank a's C column roots (rank 0)
+ *   CDA_SPLIT_COMBINE     slot index, in the gathered subtrees, of rank a's node of row b */
+#define CDA_SPLIT_SEND 0
+#define CDA_SPLIT_SEND_PIECE 1
+#define CDA_SPLIT_RECV_PIECE 2
+#define CDA_SPLIT_BLOCK 3
+#define CDA_SPLIT_GATHER_SUB 4
+#define CDA_SPLIT_GATHER_COL 5
+#define CDA_SPLIT_COMBINE 6
+int cda_split_offsets(uint32_t k, uint32_t world, int what, uint32_t n, const uint32_t *a, const uint32_t *b,
+                      uint64_t *off);
 /* Config 4 on one node: n independent squares (host buffers, as
  * cda_extend_dah_batch) split into contiguous shards over n_ctx contexts (one
  * per GPU) and run concurrently on host threads; no collective. */

@@ -34,6 +34,7 @@ def pytest_runtest_makereport(item, call):
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "gpu_failures.log"), "a") as f:
             f.write(f"==== {datetime.datetime.now().isoformat()} {item.nodeid} ({call.when})\n")
-            f.write(str(call.excinfo.getrepr(style="long")) + "\n")
+            f.write(f"{call.excinfo.typename}: {call.excinfo.value}\n")
+            f.write(str(call.excinfo.getrepr(style="short", tbfilter=True)) + "\n")
     except Exception:
         pass
