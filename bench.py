@@ -276,19 +276,39 @@ def host_pipeline_rates(ctx, k: int, d_ods, d_eds, idx, reps: int = 3) -> dict:
     t_roots = med(lambda: run(False))
     t_eds = med(lambda: run(True))
     g = golden_config4()
-    checked = matched = eds_checked = eds_matched = 0
-    if g and g.get("k") == k:
-        for j, i in enumerate(idx[:n]):
-            want = g["squares"].get(str(i))
-            if want is None:
-                continue
-            checked += 1
-            matched += int(roots[j].tobytes().hex() == want["data_root"])
-            if "eds_sha256" in want and eds_checked < 8:
-                eds_checked += 1
-                eds_matched += int(hashlib.sha256(h_eds[j].numpy().tobytes()).hexdigest() == want["eds_sha256"])
-    assert int(np.abs(status).sum()) == 0, "push-order status set on ordered input"
-    assert matched == checked and eds_matched == eds_checked, (matched, checked, eds_matched, eds_checked)
+
+    def check_roots_and_eds(eds_of):
+        checked = matched = eds_checked = eds_matched = 0
+        if g and g.get("k") == k:
+            for j, i in enumerate(idx[:n]):
+                want = g["squares"].get(str(i))
+                if want is None:
+                    continue
+                checked += 1
+                matched += int(roots[j].tobytes().hex() == want["data_root"])
+                if "eds_sha256" in want and eds_checked < 8:
+                    eds_checked += 1
+                    eds_matched += int(hashlib.sha256(eds_of(j)).hexdigest() == want["eds_sha256"])
+        assert int(np.abs(status).sum()) == 0, "push-order status set on ordered input"
+        assert matched == checked and eds_matched == eds_checked, (matched, checked, eds_matched, eds_checked)
+        return {"data_roots_checked": checked, "data_roots_matched": matched,
+                "eds_digests_checked": eds_checked, "eds_digests_matched": eds_matched}
+
+    par_check = check_roots_and_eds(lambda j: h_eds[j].numpy().tobytes())
+    # packed parity (CDA_EDS_PARITY): the caller keeps Q0 (its own shares), the
+    # device packs each chunk's parity and returns it in one linear copy; the
+    # buffer reuses h_eds's pinned storage
+    from celestia_da import _lib as _L
+    from celestia_da.da import unpack_parity
+    h_par = h_eds.view(-1)[:n * 3 * ods_b].view(n, 3 * ods_b)
+
+    def run_packed():
+        ctx.check(ctx.lib.cda_extend_dah_batch_ex(ctx.h, tptr(h_ods), k, n, tptr(h_par), _L.CDA_EDS_PARITY,
+                                                  ptr(rows), ptr(cols), ptr(roots), st))
+
+    t_par = med(run_packed)
+    packed_check = check_roots_and_eds(lambda j: unpack_parity(h_ods[j].numpy(), h_par[j].numpy().reshape(-1, SHARE))
+                                       .tobytes())
     h2d_line, d2h_line = n * ods_b / t_h2d / 1e9, par / t_d2h / 1e9
     roots_gbs, eds_gbs = n * ods_b / t_roots / 1e9, par / t_eds / 1e9
     return {"k": k, "squares": n,
@@ -297,13 +317,16 @@ def host_pipeline_rates(ctx, k: int, d_ods, d_eds, idx, reps: int = 3) -> dict:
             "eds_to_host_squares_per_s": n / t_eds, "eds_d2h_gb_per_s": eds_gbs,
             "d2h_line_gb_per_s": d2h_line, "eds_frac_of_d2h_line": eds_gbs / d2h_line,
             "bidir_line_squares_per_s": n / t_both, "eds_frac_of_bidir_line": t_both / t_eds,
-            "parity": {"data_roots_checked": checked, "data_roots_matched": matched,
-                       "eds_digests_checked": eds_checked, "eds_digests_matched": eds_matched},
+            "packed_parity_squares_per_s": n / t_par, "packed_parity_d2h_gb_per_s": par / t_par / 1e9,
+            "packed_frac_of_bidir_line": t_both / t_par, "packed_frac_of_d2h_line": t_d2h / t_par,
+            "parity": par_check, "parity_packed": packed_check,
             "note": "one cda_extend_dah_batch call over the rank's squares from page-locked host buffers "
                     "(torch pin_memory): ODS up, roots (and with the EDS: the three parity quadrants) down; "
                     "the library pipelines 32-square chunks over three streams; line rates = plain pinned "
                     "copies of the same bytes in the same run, one direction at a time; bidir line = both copies at once "
-                    "on two streams (the pipeline's own mix of ODS up and parity down)"}
+                    "on two streams (the pipeline's own mix of ODS up and parity down); packed_parity = "
+                    "cda_extend_dah_batch_ex(CDA_EDS_PARITY): the caller keeps Q0 (its shares), parity packed on the "
+                    "device and returned in one linear copy per chunk, EDS digests checked on the reassembled square"}
 
 
 def cpu_model() -> str:

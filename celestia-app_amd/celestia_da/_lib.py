@@ -37,6 +37,11 @@ CDA_ERR_COMM = -11
 CDA_SQUARE_CONSTRUCT = 0
 CDA_SQUARE_BUILD = 1
 
+# cda_extend_dah_batch_ex eds modes (include/cda.h)
+CDA_EDS_FULL = 0
+CDA_EDS_SKIP_Q0 = 1
+CDA_EDS_PARITY = 2
+
 # cda_split_offsets selectors (include/cda.h)
 CDA_SPLIT_SEND = 0
 CDA_SPLIT_SEND_PIECE = 1
@@ -58,7 +63,7 @@ EXPORTED = (
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
     "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
     "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_comm_abort", "cda_extend_dah_split", "cda_split_rows_send",
-    "cda_extend_dah_multi", "cda_split_layout", "cda_split_offsets",
+    "cda_extend_dah_multi", "cda_split_layout", "cda_split_offsets", "cda_extend_dah_batch_ex",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
 
@@ -131,6 +136,8 @@ def load():
         L.cda_extend_dah.argtypes = [ctxp, u8p, C.c_uint32, u8p, u8p, u8p, u8p]
         L.cda_extend_dah_batch.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p, u8p,
                                            C.POINTER(C.c_int32)]
+        L.cda_extend_dah_batch_ex.argtypes = [ctxp, u8p, C.c_uint32, C.c_uint32, u8p, C.c_int, u8p, u8p, u8p,
+                                              C.POINTER(C.c_int32)]
         L.cda_extend_dah_device.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.cda_reserve.argtypes = [ctxp, C.c_uint32, C.c_uint32]
         L.cda_extend_dah_inplace_device.argtypes = [ctxp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp]

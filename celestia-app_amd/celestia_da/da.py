@@ -222,6 +222,48 @@ def min_data_availability_header() -> DataAvailabilityHeader:
     return new_data_availability_header(extend_shares(min_shares()))
 
 
+def extend_dah_batch_parity(ods: np.ndarray, ctx=None, skip_q0: bool = False):
+    """cda_extend_dah_batch_ex: the batch's roots and its parity only.
+
+    skip_q0=False: packed parity (CDA_EDS_PARITY), (n, 3k^2, 512) -- per square
+    Q1 (k rows of k shares) then EDS rows k..2k-1; skip_q0=True: the full EDS
+    layout (n, 2k, 2k, 512) with Q0 left zero (CDA_EDS_SKIP_Q0).  Returns
+    (parity, rows, cols, data_roots, status)."""
+    ctx = ctx or default_context()
+    ods = np.ascontiguousarray(ods, dtype=np.uint8)
+    n = ods.shape[0]
+    k = int(round((ods.size // (n * SHARE_SIZE)) ** 0.5))
+    W = 2 * k
+    if skip_q0:
+        out = np.zeros((n, W, W, SHARE_SIZE), dtype=np.uint8)
+        mode = _lib.CDA_EDS_SKIP_Q0
+    else:
+        out = np.empty((n, 3 * k * k, SHARE_SIZE), dtype=np.uint8)
+        mode = _lib.CDA_EDS_PARITY
+    rows = np.empty((n, W, NMT_ROOT_SIZE), dtype=np.uint8)
+    cols = np.empty((n, W, NMT_ROOT_SIZE), dtype=np.uint8)
+    roots = np.empty((n, 32), dtype=np.uint8)
+    status = np.empty(n, dtype=np.int32)
+    import ctypes as C
+    rc = ctx.lib.cda_extend_dah_batch_ex(ctx.h, ptr(ods), k, n, ptr(out), mode, ptr(rows), ptr(cols), ptr(roots),
+                                         status.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc not in (_lib.CDA_OK, _lib.CDA_ERR_PUSH_ORDER):
+        ctx.check(rc)
+    return out, rows, cols, roots, status
+
+
+def unpack_parity(ods: np.ndarray, par: np.ndarray) -> np.ndarray:
+    """The whole EDS (W, W, 512) of one square from its ODS and its packed
+    parity (extend_dah_batch_parity), as a cgo caller assembles the cells."""
+    k = int(round((ods.size // SHARE_SIZE) ** 0.5))
+    W = 2 * k
+    eds = np.empty((W, W, SHARE_SIZE), dtype=np.uint8)
+    eds[:k, :k] = ods.reshape(k, k, SHARE_SIZE)
+    eds[:k, k:] = par[:k * k].reshape(k, k, SHARE_SIZE)
+    eds[k:] = par[k * k:].reshape(k, W, SHARE_SIZE)
+    return eds
+
+
 def extend_dah_batch(ods: np.ndarray, want_eds: bool = True, ctx=None):
     """Batch of n squares (n, k*k, 512) -> (eds|None, rows, cols, data_roots, status)."""
     ctx = ctx or default_context()

@@ -203,6 +203,18 @@ int cda_extend_dah_batch(cda_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t 
     });
 }
 
+int cda_extend_dah_batch_ex(cda_ctx* ctx, const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, int eds_mode,
+                            uint8_t* row_roots, uint8_t* col_roots, uint8_t* data_roots, int32_t* status) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (k == 0 || (k & (k - 1))) return not_pow2(e, k * k);
+        if (eds_mode != CDA_EDS_FULL && eds_mode != CDA_EDS_SKIP_Q0 && eds_mode != CDA_EDS_PARITY)
+            return e.fail(CDA_ERR_INVALID, "unknown eds_mode");
+        if (n == 0) return CDA_OK;
+        if (!ods || !row_roots || !col_roots || !data_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.host_extend_dah(ods, k, n, eds, row_roots, col_roots, data_roots, status, eds_mode);
+    });
+}
+
 int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t n, void* d_eds, void* d_row_roots,
                           void* d_col_roots, void* d_data_roots, int32_t* d_status, void* stream) {
     return guarded_stream(ctx, stream, [&](cda::Engine& e, hipStream_t s) -> int {

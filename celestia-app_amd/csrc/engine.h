@@ -195,8 +195,11 @@ class Engine {
                          uint8_t* d_col_roots, uint8_t* d_root, uint32_t* d_err, hipStream_t s);
 
     // Host-buffer helpers (copy in, run, copy out, synchronise).
+    // eds_mode (include/cda.h CDA_EDS_*): the whole EDS with Q0 copied on the
+    // host (FULL), the whole EDS without Q0 (SKIP_Q0: the caller's Q0 cells
+    // alias its shares), or packed parity [n][Q1 k x k | rows k..2k-1] (PARITY).
     int host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
-                        uint8_t* roots, int32_t* status);
+                        uint8_t* roots, int32_t* status, int eds_mode = 0);
     int host_extend(const uint8_t* ods, uint32_t k, uint8_t* eds);
     int host_dah(const uint8_t* eds, uint32_t k, uint8_t* rows, uint8_t* cols, uint8_t* root);
     int host_rs(const uint8_t* data, uint32_t k, uint32_t len, uint32_t n, uint8_t* parity);
@@ -311,8 +314,9 @@ class Engine {
     // copy_out_ while stream_ hashes (ev_rs_: RS done, ev_out_: copies done)
     hipStream_t copy_out_ = nullptr;
     hipEvent_t ev_rs_ = nullptr, ev_out_ = nullptr;
+    // eds_mode PARITY: d_par = device staging of n packed parity squares
     int enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
-                           hipEvent_t ready, hipEvent_t done);
+                           hipEvent_t ready, hipEvent_t done, int eds_mode = 0, uint8_t* d_par = nullptr);
     // Big host-buffer batches (host_extend_dah, n > 2 chunks): chunks of
     // squares through a ring of kPipeSlots device slots, H2D on copy_in_,
     // extension + hashing on stream_, parity D2H on copy_out_, so chunk i+1
@@ -323,7 +327,8 @@ class Engine {
                pipe_comp_[kPipeSlots] = {};
     uint32_t host_pipe_chunk_ = 0;   // CDA_HOST_PIPE_CHUNK: squares per chunk (0 = auto: ~256 MiB of ODS)
     int host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
-                      uint8_t* roots, int32_t* status, uint32_t chunk);
+                      uint8_t* roots, int32_t* status, uint32_t chunk, int eds_mode);
+    DevBuf h_par_;   // packed-parity staging (eds_mode PARITY)
     static void copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds);
     hipEvent_t order_ev_ = nullptr;   // end of the last call's GPU work
     bool order_used_ = false;

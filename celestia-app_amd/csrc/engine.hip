@@ -993,13 +993,47 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
     for (auto& x : th) x.join();
 }
 
+// Packed parity of n squares (eds_mode PARITY): per square Q1 as k rows of k
+// shares, then EDS rows k..2k-1 (Q2 | Q3) whole -- 3 k^2 shares, contiguous,
+// so the chunk's parity leaves in ONE linear device-to-host copy instead of a
+// strided Q1 copy and a linear Q2 | Q3 copy per square (each copy costs a
+// ~30 us turnaround on the DMA engine, profiles/r04/host_pipe_trace.txt).
+// One thread per 16 bytes.
+__global__ __launch_bounds__(256) void pack_parity_kernel(const uint8_t* __restrict__ eds, uint8_t* __restrict__ par,
+                                                         uint32_t k, uint64_t total16) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total16) return;
+    constexpr uint32_t V = kShare / 16;
+    const uint64_t W = 2 * (uint64_t)k, per_sq = 3 * (uint64_t)k * k * V;
+    const uint64_t sq = i / per_sq, j = i % per_sq;
+    const uint64_t q1 = (uint64_t)k * k * V;
+    uint64_t src;   // in uint4 units within the square
+    if (j < q1) {
+        const uint64_t cell = j / V, r = cell / k, c = cell % k;
+        src = (r * W + k + c) * V + j % V;
+    } else {
+        src = (uint64_t)k * W * V + (j - q1);
+    }
+    reinterpret_cast<uint4*>(par)[i] = reinterpret_cast<const uint4*>(eds + sq * W * W * kShare)[src];
+}
+
 int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* eds, hipStream_t from,
-                               hipEvent_t ready, hipEvent_t done) {
+                               hipEvent_t ready, hipEvent_t done, int eds_mode, uint8_t* d_par) {
     const size_t W = 2 * (size_t)k, sq_b = W * W * kShare, half = k * W * kShare;
     int rc;
     if ((rc = check(hipEventRecord(ready, from), "hipEventRecord"))) return rc;
     if ((rc = check(hipStreamWaitEvent(copy_out_, ready, 0), "hipStreamWaitEvent"))) return rc;
-    if (host_full_d2h_) {   // the whole EDS back as one contiguous copy (Q0 included)
+    if (eds_mode == CDA_EDS_PARITY) {
+        // pack on the copy stream (beside the hashing), then one linear copy
+        const size_t par_b = (size_t)n * 3 * k * k * kShare;
+        const uint64_t total16 = par_b / 16;
+        hipLaunchKernelGGL(pack_parity_kernel, dim3((uint32_t)((total16 + 255) / 256)), dim3(256), 0, copy_out_, d_eds,
+                           d_par, k, total16);
+        if ((rc = check(hipGetLastError(), "pack parity"))) return rc;
+        if ((rc = check(hipMemcpyAsync(eds, d_par, par_b, hipMemcpyDeviceToHost, copy_out_), "D2H parity"))) return rc;
+        return check(hipEventRecord(done, copy_out_), "hipEventRecord");
+    }
+    if (host_full_d2h_ && eds_mode == CDA_EDS_FULL) {   // the whole EDS back as one contiguous copy (Q0 included)
         if ((rc = check(hipMemcpyAsync(eds, d_eds, n * sq_b, hipMemcpyDeviceToHost, copy_out_), "D2H EDS"))) return rc;
         return check(hipEventRecord(done, copy_out_), "hipEventRecord");
     }
@@ -1032,12 +1066,15 @@ int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uin
 // run at once (PCIe is full duplex); the host copies Q0 (= the caller's ODS)
 // on its own threads meanwhile.
 int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
-                          uint8_t* roots, int32_t* status, uint32_t c) {
+                          uint8_t* roots, int32_t* status, uint32_t c, int eds_mode) {
     const uint32_t W = 2 * k;
     const size_t ods_sq = (size_t)k * k * kShare, eds_sq = (size_t)W * W * kShare, root_sq = (size_t)W * kNode;
+    const bool packed = eds && eds_mode == CDA_EDS_PARITY;
+    const size_t out_sq = packed ? 3 * ods_sq : eds_sq;   // bytes per square of the caller's eds buffer
     int rc;
     if ((rc = check(h_ods_.ensure(kPipeSlots * c * ods_sq), "hipMalloc"))) return rc;
     if ((rc = check(h_eds_.ensure(kPipeSlots * c * eds_sq), "hipMalloc"))) return rc;
+    if (packed && (rc = check(h_par_.ensure(kPipeSlots * c * 3 * ods_sq), "hipMalloc"))) return rc;
     if ((rc = check(h_rows_.ensure(n * root_sq), "hipMalloc"))) return rc;
     if ((rc = check(h_cols_.ensure(n * root_sq), "hipMalloc"))) return rc;
     if ((rc = check(h_roots_.ensure((size_t)n * 32), "hipMalloc"))) return rc;
@@ -1047,7 +1084,7 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
     if ((rc = check(hipEventRecord(pipe_comp_[0], s), "hipEventRecord"))) return rc;
     if ((rc = check(hipStreamWaitEvent(copy_in_, pipe_comp_[0], 0), "hipStreamWaitEvent"))) return rc;
     HostPin pin_ods(host_register_, ods, (size_t)n * ods_sq, copy_in_, s),
-        pin_eds(host_register_, eds, (size_t)n * eds_sq, s, copy_out_);
+        pin_eds(host_register_, eds, (size_t)n * out_sq, s, copy_out_);
     uint32_t* err = err_buf_.as<uint32_t>();
     for (uint32_t i = 0, i0 = 0; i0 < n; i++, i0 += c) {
         const uint32_t m = std::min(c, n - i0), slot = i % kPipeSlots;
@@ -1062,7 +1099,8 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
         if (eds && i >= kPipeSlots && (rc = check(hipStreamWaitEvent(s, pipe_d2h_[slot], 0), "hipStreamWaitEvent")))
             return rc;
         if ((rc = enqueue_extend(d_ods, k, m, d_eds, s, err + i0))) return rc;
-        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * eds_sq, s, pipe_rs_[slot], pipe_d2h_[slot])))
+        if (eds && (rc = enqueue_parity_d2h(d_eds, k, m, eds + i0 * out_sq, s, pipe_rs_[slot], pipe_d2h_[slot],
+                                            eds_mode, packed ? h_par_.as<uint8_t>() + slot * c * 3 * ods_sq : nullptr)))
             return rc;
         if ((rc = enqueue_dah(d_eds, k, m, h_rows_.as<uint8_t>() + i0 * root_sq, h_cols_.as<uint8_t>() + i0 * root_sq,
                               h_roots_.as<uint8_t>() + (size_t)i0 * 32, err + i0, nullptr, s, true)))
@@ -1078,7 +1116,7 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
     if ((rc = check(hipMemcpyAsync(roots, h_roots_.ptr, (size_t)n * 32, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
     std::vector<uint32_t> words(n);
     if ((rc = check(hipMemcpyAsync(words.data(), err, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H"))) return rc;
-    if (eds && !host_full_d2h_) copy_q0(ods, k, n, eds);   // host work while the GPU runs
+    if (eds && eds_mode == CDA_EDS_FULL && !host_full_d2h_) copy_q0(ods, k, n, eds);   // host work while the GPU runs
     if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
     if (eds && (rc = check(hipStreamSynchronize(copy_out_), "hipStreamSynchronize"))) return rc;
     if (status)
@@ -1087,14 +1125,17 @@ int Engine::host_pipeline(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* e
 }
 
 int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds, uint8_t* rows, uint8_t* cols,
-                            uint8_t* roots, int32_t* status) {
+                            uint8_t* roots, int32_t* status, int eds_mode) {
+    if (eds_mode != CDA_EDS_FULL && eds_mode != CDA_EDS_SKIP_Q0 && eds_mode != CDA_EDS_PARITY)
+        return fail(CDA_ERR_INVALID, "unknown eds_mode");
     const uint32_t W = 2 * k;
     const size_t ods_b = (size_t)n * k * k * kShare, eds_b = (size_t)n * W * W * kShare;
     const size_t roots_b = (size_t)n * W * kNode;
+    const bool packed = eds && eds_mode == CDA_EDS_PARITY;
     {   // big batches: the chunk pipeline (chunk ~ 256 MiB of ODS: 32 squares at k = 128)
         const size_t ods_sq = (size_t)k * k * kShare;
         const uint32_t c = host_pipe_chunk_ ? host_pipe_chunk_ : (uint32_t)std::max<size_t>(1, (256u << 20) / ods_sq);
-        if (n > 2 * c) return host_pipeline(ods, k, n, eds, rows, cols, roots, status, c);
+        if (n > 2 * c) return host_pipeline(ods, k, n, eds, rows, cols, roots, status, c, eds_mode);
     }
     int rc;
     if ((rc = check(h_ods_.ensure(ods_b), "hipMalloc"))) return rc;
@@ -1103,9 +1144,10 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     if ((rc = check(h_cols_.ensure(roots_b), "hipMalloc"))) return rc;
     if ((rc = check(h_roots_.ensure((size_t)n * 32), "hipMalloc"))) return rc;
     if ((rc = check(err_buf_.ensure((size_t)n * 4), "hipMalloc"))) return rc;
+    if (packed && (rc = check(h_par_.ensure(3 * ods_b), "hipMalloc"))) return rc;
     hipStream_t s = stream_;
     HostPin pin_ods(host_register_, ods, ods_b, stream_, copy_out_),
-        pin_eds(host_register_, eds, eds_b, stream_, copy_out_);
+        pin_eds(host_register_, eds, packed ? 3 * ods_b : eds_b, stream_, copy_out_);
     // With the EDS going back, the batch moves in chunks: chunk i+1's ODS goes
     // up while chunk i's parity comes down (PCIe is full duplex); without
     // chunks every H2D would precede every D2H.  CDA_HOST_CHUNK (squares,
@@ -1121,8 +1163,9 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
         if ((rc = enqueue_extend(h_ods_.as<uint8_t>() + i0 * ods_sq, k, m, h_eds_.as<uint8_t>() + i0 * eds_sq, s,
                                  err_buf_.as<uint32_t>() + i0)))
             return rc;
-        if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>() + i0 * eds_sq, k, m, eds + i0 * eds_sq, s, ev_rs_,
-                                            ev_out_)))
+        if (eds && (rc = enqueue_parity_d2h(h_eds_.as<uint8_t>() + i0 * eds_sq, k, m,
+                                            eds + i0 * (packed ? 3 * ods_sq : eds_sq), s, ev_rs_, ev_out_, eds_mode,
+                                            packed ? h_par_.as<uint8_t>() + i0 * 3 * ods_sq : nullptr)))
             return rc;
     }
     if ((rc = enqueue_dah(h_eds_.as<uint8_t>(), k, n, h_rows_.as<uint8_t>(), h_cols_.as<uint8_t>(),
@@ -1134,7 +1177,7 @@ int Engine::host_extend_dah(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t*
     std::vector<uint32_t> err(n);
     if ((rc = check(hipMemcpyAsync(err.data(), err_buf_.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H")))
         return rc;
-    if (eds && !host_full_d2h_) copy_q0(ods, k, n, eds);   // host work while the GPU runs
+    if (eds && eds_mode == CDA_EDS_FULL && !host_full_d2h_) copy_q0(ods, k, n, eds);   // host work while the GPU runs
     if ((rc = check(hipStreamSynchronize(s), "hipStreamSynchronize"))) return rc;
     if (eds && (rc = check(hipEventSynchronize(ev_out_), "hipEventSynchronize"))) return rc;
     if (status)

@@ -131,6 +131,26 @@ int cda_extend_dah(cda_ctx *ctx, const uint8_t *ods, uint32_t n_shares, uint8_t 
 int cda_extend_dah_batch(cda_ctx *ctx, const uint8_t *ods, uint32_t k, uint32_t n, uint8_t *eds, uint8_t *row_roots,
                          uint8_t *col_roots, uint8_t *data_roots, int32_t *status);
 
+/* cda_extend_dah_batch with a choice of what goes back into eds (NULL: roots
+ * only, as before):
+ *   CDA_EDS_FULL     eds = n*(2k)^2*512, the whole EDS (= cda_extend_dah_batch);
+ *                    the library copies Q0 from ods on host threads;
+ *   CDA_EDS_SKIP_Q0  the same buffer, Q0 left untouched: a cgo caller that
+ *                    wraps the EDS with rsmt2d.ImportExtendedDataSquare points
+ *                    the Q0 cells at its own shares (it holds them already),
+ *                    which saves the host copy of Q0;
+ *   CDA_EDS_PARITY   eds = n*3*k^2*512 packed parity: per square Q1 as k rows
+ *                    of k shares ([k][k][512]), then EDS rows k..2k-1 whole
+ *                    ([k][2k][512]); Q0 is the caller's ODS.  The device packs
+ *                    each chunk and returns it in one linear copy.
+ * Reference: pkg/da/data_availability_header.go:65-75 (ExtendShares returns
+ * the EDS whose Q0 cells are the input shares). */
+#define CDA_EDS_FULL 0
+#define CDA_EDS_SKIP_Q0 1
+#define CDA_EDS_PARITY 2
+int cda_extend_dah_batch_ex(cda_ctx *ctx, const uint8_t *ods, uint32_t k, uint32_t n, uint8_t *eds, int eds_mode,
+                            uint8_t *row_roots, uint8_t *col_roots, uint8_t *data_roots, int32_t *status);
+
 /* Device-resident batch: every pointer is device memory on ctx's device;
  * stream is a hipStream_t; NULL is HIP's default (null) stream, the one a
  * PyTorch/Go caller enqueues on by default -- NOT the context's private
