@@ -404,7 +404,7 @@ struct SigPlan {
     uint8_t a[kPlanSignals], b[kPlanSignals], c[kPlanSignals];   // c = 0xFF: a pair
     int n;                 // derived signals in use
     uint32_t base[16];     // row masks over 16 + kPlanSignals signals
-    uint32_t lane[4][16];
+    uint32_t lane[6][16];   // up to 6 masked lane terms (tools/probes/rs16_per_wave.patch)
     uint32_t wave[2][16];
 };
 // ops of a row of t signals: x ^= sum (base / wave) or x ^= sum & m (lane)
@@ -415,8 +415,8 @@ constexpr int plan_row_ops(uint32_t msk, bool masked) {
 }
 constexpr SigPlan make_plan(uint32_t c0, const uint32_t* tl, int nl, const uint32_t* tw, int nw) {
     SigPlan P{};
-    uint32_t rows[16 * 7] = {};
-    bool msk[16 * 7] = {};
+    uint32_t rows[16 * 9] = {};
+    bool msk[16 * 9] = {};
     int nr = 0;
     auto add = [&](uint32_t c, bool masked) {
         const Net n = make_net(c);
@@ -490,7 +490,8 @@ constexpr SigPlan make_plan(uint32_t c0, const uint32_t* tl, int nl, const uint3
 }
 template <int LOGK, bool INV, int b, int NL, int LB, int NWB, int WB>
 constexpr SigPlan layer_plan(uint32_t c0) {
-    uint32_t tl[4] = {}, tw[2] = {};
+    uint32_t tl[6] = {}, tw[2] = {};
+    static_assert(NL <= 6 && NWB <= 2, "SigPlan holds 6 lane and 2 wave terms");
     for (int l = 0; l < NL; l++) tl[l] = tbasis(b, LB + l);
     for (int w = 0; w < NWB; w++) tw[w] = tbasis(b, WB + w);
     return make_plan(c0, tl, NL, tw, NWB);
@@ -505,14 +506,46 @@ B16_HD void plan_row_masked(uint32_t& x, const uint32_t* S, uint32_t m) {
     if constexpr (MSK != 0) x = xor_and(x, xor_sel<MSK>(S), m);
 }
 
+// A layer's lane masks: an array (m[l]) or a functor that derives mask L
+// where it is needed (LaneMask: no long-lived mask registers).
+template <int L, class M>
+B16_HD uint32_t mask_at(const M& m) {
+    if constexpr (std::is_pointer_v<M> || std::is_array_v<M>)
+        return m[L];
+    else
+        return m.template get<L>();
+}
+// All-ones when bit BASE + L of the lane index is set: one v_bfe_i32 (opaque
+// asm, so it is neither hoisted nor kept alive across the networks).
+template <int BASE>
+struct LaneMask {
+    uint32_t lane;
+    template <int L>
+    B16_HD uint32_t get() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        uint32_t v;
+        asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(v) : "v"(lane), "n"(BASE + L));
+        return v;
+#else
+        return 0u - ((lane >> (BASE + L)) & 1);
+#endif
+    }
+};
+
+// the masks of lane bits from BY up: m + BY for an array, BASE + BY for LaneMask
+template <int BY>
+B16_HD const uint32_t* shifted(const uint32_t* m) { return m + BY; }
+template <int BY, int BASE>
+B16_HD LaneMask<BASE + BY> shifted(const LaneMask<BASE>& m) { return LaneMask<BASE + BY>{m.lane}; }
+
 // One layer over the 8 units: unit distance D, shard bit b, the unit index
 // holding shard bits from SH up (group bits of unit i: (i & ~(2D-1)) << SH),
 // NL masked lane terms (shard bits LB..), NWB uniform wave terms (bits WB..).
 // Per butterfly the shared signals of y are formed once and every term reads
 // them; the wave terms are uniform branches.
 #ifndef CDA_BS16_PAIR_SIGNALS
-template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB>
-B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
+template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB, class M>
+B16_HD void layer8(uint32_t* R, const M& m, uint32_t u) {
     sfor<0, 8, 1>([&](auto ii) {
         constexpr int i = decltype(ii)::value;
         if constexpr ((i & D) == 0) {
@@ -540,9 +573,10 @@ B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
             });
             sfor<0, NL, 1>([&](auto ll) {
                 constexpr int l = decltype(ll)::value;
+                const uint32_t mk = mask_at<l>(m);
                 sfor<0, 16, 1>([&](auto rr) {
                     constexpr int r = decltype(rr)::value;
-                    plan_row_masked<P.lane[l][r]>(x[r], S, m[l]);
+                    plan_row_masked<P.lane[l][r]>(x[r], S, mk);
                 });
             });
             sfor<0, NWB, 1>([&](auto ww) {
@@ -564,8 +598,8 @@ B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
     });
 }
 #else
-template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB>
-B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
+template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB, class M>
+B16_HD void layer8(uint32_t* R, const M& m, uint32_t u) {
     sfor<0, 8, 1>([&](auto ii) {
         constexpr int i = decltype(ii)::value;
         if constexpr ((i & D) == 0) {
@@ -581,7 +615,7 @@ B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
             mul_add_s<C0>(x, S);
             sfor<0, NL, 1>([&](auto ll) {
                 constexpr int l = decltype(ll)::value;
-                mul_add_masked_s<tbasis(b, LB + l)>(x, S, m[l]);
+                mul_add_masked_s<tbasis(b, LB + l)>(x, S, mask_at<l>(m));
             });
             sfor<0, NWB, 1>([&](auto ww) {
                 constexpr int w = decltype(ww)::value;
@@ -598,30 +632,30 @@ B16_HD void layer8(uint32_t* R, const uint32_t* m, uint32_t u) {
 }
 #endif
 // LOW layer b (0..2): unit = shard bits 0..2, lane bits 3..6 (m[0..3]), wave bits 7..
-template <int LOGK, bool INV, int b>
-B16_HD void low_layer(uint32_t* R, const uint32_t* m, uint32_t u) {
+template <int LOGK, bool INV, int b, class M>
+B16_HD void low_layer(uint32_t* R, const M& m, uint32_t u) {
     layer8<LOGK, INV, b, 1 << b, 0, 4, 3, LOGK - 7, 7>(R, m, u);
 }
 // M1 layer b (3..5): unit = shard bits 3..5, lane bit 6 (m[3]), wave bits 7..
-template <int LOGK, bool INV, int b>
-B16_HD void m1_layer(uint32_t* R, const uint32_t* m, uint32_t u) {
-    layer8<LOGK, INV, b, 1 << (b - 3), 3, 1, 6, LOGK - 7, 7>(R, m + 3, u);
+template <int LOGK, bool INV, int b, class M>
+B16_HD void m1_layer(uint32_t* R, const M& m, uint32_t u) {
+    layer8<LOGK, INV, b, 1 << (b - 3), 3, 1, 6, LOGK - 7, 7>(R, shifted<3>(m), u);
 }
 // M2 layer b (LOGK-3..LOGK-1): unit = shard bits LOGK-3.., no lane / wave terms
 template <int LOGK, bool INV, int b>
 B16_HD void m2_layer(uint32_t* R) {
-    layer8<LOGK, INV, b, 1 << (b - (LOGK - 3)), LOGK - 3, 0, 0, 0, 0>(R, nullptr, 0);
+    layer8<LOGK, INV, b, 1 << (b - (LOGK - 3)), LOGK - 3, 0, 0, 0, 0>(R, (const uint32_t*)nullptr, 0);
 }
 // The phases in encode order (leopard.go encode: IFFT over the k data shards
 // at coset k, then FFT to the k parity shards):
-template <int LOGK>
-B16_HD void phase_low_ifft(uint32_t* R, const uint32_t* m, uint32_t u) {
+template <int LOGK, class M>
+B16_HD void phase_low_ifft(uint32_t* R, const M& m, uint32_t u) {
     low_layer<LOGK, true, 0>(R, m, u);
     low_layer<LOGK, true, 1>(R, m, u);
     low_layer<LOGK, true, 2>(R, m, u);
 }
-template <int LOGK>
-B16_HD void phase_m1_ifft(uint32_t* R, const uint32_t* m, uint32_t u) {   // layers 3..5
+template <int LOGK, class M>
+B16_HD void phase_m1_ifft(uint32_t* R, const M& m, uint32_t u) {   // layers 3..5
     m1_layer<LOGK, true, 3>(R, m, u);
     m1_layer<LOGK, true, 4>(R, m, u);
     m1_layer<LOGK, true, 5>(R, m, u);
@@ -631,12 +665,12 @@ B16_HD void phase_m2(uint32_t* R) {   // IFFT 6..LOGK-1, FFT LOGK-1..LOGK-3
     sfor<6, LOGK, 1>([&](auto bb) { m2_layer<LOGK, true, decltype(bb)::value>(R); });
     sfor<0, 3, 1>([&](auto bb) { m2_layer<LOGK, false, LOGK - 1 - decltype(bb)::value>(R); });
 }
-template <int LOGK>
-B16_HD void phase_m1_fft(uint32_t* R, const uint32_t* m, uint32_t u) {   // layers LOGK-4..3
+template <int LOGK, class M>
+B16_HD void phase_m1_fft(uint32_t* R, const M& m, uint32_t u) {   // layers LOGK-4..3
     sfor<0, LOGK - 6, 1>([&](auto bb) { m1_layer<LOGK, false, LOGK - 4 - decltype(bb)::value>(R, m, u); });
 }
-template <int LOGK>
-B16_HD void phase_low_fft(uint32_t* R, const uint32_t* m, uint32_t u) {
+template <int LOGK, class M>
+B16_HD void phase_low_fft(uint32_t* R, const M& m, uint32_t u) {
     low_layer<LOGK, false, 2>(R, m, u);
     low_layer<LOGK, false, 1>(R, m, u);
     low_layer<LOGK, false, 0>(R, m, u);

@@ -73,7 +73,14 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     rs_err_init(job);
     extern __shared__ u32x4 X[];
     const uint32_t tid = threadIdx.x, lane = tid & 63, b4 = lane & 3, jl = lane >> 2;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // The wave -> shard-bit mapping is rotated per workgroup: the wave with
+    // wave bits 11 runs both uniform-branch terms of every LOW / M1 butterfly,
+    // the one with 00 none, and the waves of a workgroup go to the SIMDs of a
+    // CU in index order, so without the rotation one SIMD of every CU runs the
+    // heaviest wave of each co-resident workgroup.  Round 5, interleaved A/B
+    // (profiles/r05/rs16_ab.txt): RS per k = 512 square 0.320 -> 0.312 ms
+    // (batch 1), 0.271 -> 0.257 (4), 0.257 -> 0.250 (16).
+    const uint32_t w = __builtin_amdgcn_readfirstlane(((tid >> 6) + (blockIdx.x >> 1) + blockIdx.y) & (NW - 1));
     const uint32_t cw = blockIdx.x >> 1, half = blockIdx.x & 1;
     const bool s1 = job.n_seg > 1 && cw >= job.seg[0].n_cw;
     const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
@@ -115,9 +122,13 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
         });
     }
     bs16::sfor<0, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
+#ifdef CDA_BS16_LANEMASK
+    const bs16::LaneMask<0> m{jl};   // A/B: masks derived where used (4 fewer long-lived VGPRs)
+#else
     uint32_t m[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) m[i] = 0u - ((jl >> i) & 1);
+#endif
     bs16::phase_low_ifft<LOGK>(R, m, w);
 
     // ---- exchanges ------------------------------------------------------------

@@ -35,6 +35,9 @@ def pytest_runtest_makereport(item, call):
         with open(os.path.join(d, "gpu_failures.log"), "a") as f:
             f.write(f"==== {datetime.datetime.now().isoformat()} {item.nodeid} ({call.when})\n")
             f.write(f"{call.excinfo.typename}: {call.excinfo.value}\n")
-            f.write(str(call.excinfo.getrepr(style="short", tbfilter=True)) + "\n")
+            for e in call.excinfo.traceback:   # this repository's frames only
+                path = str(e.path)
+                if path.startswith(ROOT) and "/site-packages/" not in path:
+                    f.write(f"  {os.path.relpath(path, ROOT)}:{e.lineno + 1}: {str(e.statement).strip()}\n")
     except Exception:
         pass

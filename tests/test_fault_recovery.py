@@ -159,8 +159,8 @@ def test_host_pipeline_matches_serial(ctx, chunk, n):
         for a, b in zip(ref, got):
             assert np.array_equal(a, b)
         assert [bool(x) for x in got[4] != 0] == [i == bad for i in range(n)]
-        want = _oracle_roots(ods)
-        assert [bytes(got[3][i]) for i in range(n) if i != bad] == [want[i] for i in range(n) if i != bad]
+        ok = [i for i in range(n) if i != bad]
+        assert [bytes(got[3][i]) for i in ok] == _oracle_roots(ods[ok])
         e_eds = coracle.extend_dah(ods[-1])[0]
         assert np.array_equal(got[0][-1].reshape(-1, 512), e_eds)
         no_eds = da.extend_dah_batch(ods, want_eds=False, ctx=pc)

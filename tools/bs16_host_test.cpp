@@ -2,6 +2,7 @@
 // against the table build leo_build<16> (leopard_tables.h): field products, the
 // whole skew vector, the networks, the signal plans (make_plan) and the block <-> planes transpose.
 // Build: g++ -O2 -std=c++20 -I celestia-app_amd/csrc tools/bs16_host_test.cpp -o /tmp/bs16_host_test
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
