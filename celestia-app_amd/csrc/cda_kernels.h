@@ -71,11 +71,6 @@ struct CellGrid {
     uint64_t sq;            // bytes per square
     uint32_t rows, cols, row_stride;
     uint32_t row0, col0, k;
-    // leaf slots of a sub-grid inside a bigger slot grid (launch_leaves):
-    // slot of cell (r, c) of square y at y * slot_sq + r * slot_stride + c
-    // (0 = the grid's own rows * cols / cols)
-    uint32_t slot_stride = 0;
-    uint64_t slot_sq = 0;
 };
 
 // NMT leaf hashing: one 96-B leaf slot per grid cell, slots[y][r][c].  Also

@@ -170,10 +170,8 @@ class Engine {
                        uint32_t* err_init = nullptr);
     // Roots + data root of existing EDSs.
     // err_ready: d_err already holds ~0 words (enqueue_extend's err_init).
-    // leaves_done: the leaf slots are already hashed (enqueue_extend_dah_overlap)
     int enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots,
-                    uint32_t* d_err, int32_t* d_status, hipStream_t s, bool err_ready = false,
-                    bool leaves_done = false);
+                    uint32_t* d_err, int32_t* d_status, hipStream_t s, bool err_ready = false);
     int enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uint32_t len, uint32_t n, hipStream_t s);
 
     // Config 5: one square split across ranks (cda_split_* in include/cda.h).
@@ -356,17 +354,7 @@ class Engine {
     int dah_prepare(uint32_t W, uint32_t n, uint32_t* d_err, hipStream_t s);
     void dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&f)[2]);
     int dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
-                  const Forest (&f)[2], Forest (&post)[2], hipStream_t s, bool subtrees = false,
-                  bool leaves_done = false);
-    // Small batches: the leaves of each quadrant hashed on aux_stream_ as soon
-    // as the quadrant exists -- Q0 beside the RS Q0 launch, Q1 and Q2 beside
-    // the RS Q3 launch -- filling the CU slots the RS launches' last partial
-    // rounds leave idle (CDA_LEAF_OVERLAP: squares per call up to which it is
-    // used, 0 = off).
-    int enqueue_extend_dah_overlap(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,
-                                   uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err, int32_t* d_status,
-                                   hipStream_t s);
-    uint32_t leaf_overlap_ = 0;
+                  const Forest (&f)[2], Forest (&post)[2], hipStream_t s, bool subtrees = false);
     int dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const Forest (&f)[2], uint8_t* d_roots,
                    uint32_t* d_err, int32_t* d_status, hipStream_t s);
     int enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds, uint8_t* d_rows,

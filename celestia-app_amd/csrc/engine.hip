@@ -229,7 +229,6 @@ int Engine::init() {
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_FAULT")) fault_ = env;
-    if (const char* env = getenv("CDA_LEAF_OVERLAP")) leaf_overlap_ = (uint32_t)strtoul(env, nullptr, 10);
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -493,18 +492,16 @@ void Engine::dah_forests(uint32_t W, uint8_t* d_rows, uint8_t* d_cols, Forest (&
 // [i0, i0 + m).  f: the batch's forests from dah_forests; on return `post`
 // describes (for the whole batch) the level the chunk stopped at.
 int Engine::dah_chunk(const uint8_t* d_eds, uint32_t k, uint32_t i0, uint32_t m, uint32_t stop, uint32_t* d_err,
-                      const Forest (&f)[2], Forest (&post)[2], hipStream_t s, bool subtrees, bool leaves_done) {
+                      const Forest (&f)[2], Forest (&post)[2], hipStream_t s, bool subtrees) {
     const uint32_t W = 2 * k;
     const uint64_t slots_sq = (uint64_t)W * W * kSlot, eds_sq = (uint64_t)W * W * kShare;
     int rc;
-    if (!leaves_done) {
-        mark_begin(kStageLeaves, s);
-        const CellGrid g{d_eds + i0 * eds_sq, eds_sq, W, W, W, 0, 0, k};
-        if ((rc = check(launch_leaves(g, m, leaf_.as<uint8_t>() + i0 * slots_sq, d_err + i0, true, true, s),
-                        "leaf hashing")))
-            return rc;
-        mark_end(s);
-    }
+    mark_begin(kStageLeaves, s);
+    const CellGrid g{d_eds + i0 * eds_sq, eds_sq, W, W, W, 0, 0, k};
+    if ((rc = check(launch_leaves(g, m, leaf_.as<uint8_t>() + i0 * slots_sq, d_err + i0, true, true, s),
+                    "leaf hashing")))
+        return rc;
+    mark_end(s);
     Forest fc[2] = {f[0], f[1]};
     for (int i = 0; i < 2; i++) {
         fc[i].in += i0 * fc[i].in_sq;
@@ -591,8 +588,7 @@ int Engine::dah_finish(uint32_t k, uint32_t i0, uint32_t n, uint32_t from, const
 }
 
 int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d_rows, uint8_t* d_cols,
-                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s, bool err_ready,
-                        bool leaves_done) {
+                        uint8_t* d_roots, uint32_t* d_err, int32_t* d_status, hipStream_t s, bool err_ready) {
     if (!pow2(k) || k > 1024) return fail(CDA_ERR_INVALID, "square width must be a power of two <= 1024");
     const uint32_t W = 2 * k;
     int rc;
@@ -642,7 +638,7 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
                 }
             }
             Forest pp[2];
-            rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q, true, leaves_done);
+            rc = dah_chunk(d_eds, k, i0, i1 - i0, stop, d_err, f, pp, q, true);
             if (!rc) rc = dah_finish(k, i0, i1 - i0, stop, pp, d_roots, d_err, d_status, q);
             if (!rc && p && fault_at("dah_part"))
                 rc = fail(CDA_ERR_DEVICE, "enqueue_dah: injected fault after a side part's hashing (CDA_FAULT=dah_part)");
@@ -669,7 +665,7 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
         }
         return err;
     }
-    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s, true, leaves_done))) return rc;
+    if ((rc = dah_chunk(d_eds, k, 0, n, stop, d_err, f, post, s, true))) return rc;
     return dah_finish(k, 0, n, stop, post, d_roots, d_err, d_status, s);
 }
 
@@ -750,77 +746,9 @@ int Engine::enqueue_split_combine(const uint8_t* d_row_sub, uint32_t parts, uint
     return check(launch_data_root(rs, 2 * W, 1, d_root, s), "data root");
 }
 
-int Engine::enqueue_extend_dah_overlap(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds,
-                                       uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err,
-                                       int32_t* d_status, hipStream_t s) {
-    const uint32_t W = 2 * k;
-    const uint64_t eds_sq = (uint64_t)W * W * kShare, slots_sq = (uint64_t)W * W * kSlot;
-    int rc;
-    if ((rc = dah_prepare(W, n, d_err, s))) return rc;   // scratch + push-order words (~0) on s
-    hipStream_t q = aux_stream_;
-    hipEvent_t ev_go = sync_event(0), ev_q0 = sync_event(1), ev_leaves = sync_event(2);
-    if (!ev_go || !ev_q0 || !ev_leaves) return fail(CDA_ERR_DEVICE, "hipEventCreate failed");
-    // Q0's leaves read the ODS where it lies: in Q0 of the EDS (in place), or
-    // the packed ODS (row stride k) while the first RS launch copies it
-    if ((rc = check(hipEventRecord(ev_go, s), "hipEventRecord"))) return rc;
-    int err = CDA_OK;
-    bool q_used = false;
-    auto leaves = [&](uint32_t row0, uint32_t col0, uint32_t rows, uint32_t cols) -> int {
-        const bool from_ods = d_ods && row0 == 0 && col0 == 0;
-        CellGrid g = from_ods ? CellGrid{d_ods, (uint64_t)k * k * kShare, rows, cols, k, 0, 0, k}
-                              : CellGrid{d_eds + ((uint64_t)row0 * W + col0) * kShare, eds_sq, rows, cols, W, row0,
-                                         col0, k};
-        g.slot_stride = W;
-        g.slot_sq = (uint64_t)W * W;
-        uint8_t* slots = leaf_.as<uint8_t>() + ((uint64_t)row0 * W + col0) * kSlot;
-        const bool q0 = row0 == 0 && col0 == 0;   // only Q0 cells take part in the push-order check
-        return check(launch_leaves(g, n, slots, d_err, q0, q0, q), "leaf hashing");
-    };
-    do {
-        if ((err = check(hipStreamWaitEvent(q, ev_go, 0), "hipStreamWaitEvent"))) break;
-        q_used = true;
-        if ((err = leaves(0, 0, k, k))) break;   // beside RS Q0
-        mark_begin(kStageRsQ0, s);
-        RsJob j0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
-        if ((err = check(launch_rs(j0, k, n, gf16(k), s), "rs Q0"))) break;
-        mark_end(s);
-        if ((err = check(hipEventRecord(ev_q0, s), "hipEventRecord"))) break;
-        if ((err = check(hipStreamWaitEvent(q, ev_q0, 0), "hipStreamWaitEvent"))) break;
-        if ((err = leaves(0, k, k, k))) break;   // Q1, beside RS Q3
-        if ((err = leaves(k, 0, k, k))) break;   // Q2
-        mark_begin(kStageRsQ3, s);
-        if ((err = check(launch_rs(square_job_q3(d_eds, k), k, n, gf16(k), s), "rs Q3"))) break;
-        mark_end(s);
-        mark_begin(kStageLeaves, s);
-        {   // Q3 on s, after its RS
-            CellGrid g{d_eds + ((uint64_t)k * W + k) * kShare, eds_sq, k, k, W, k, k, k};
-            g.slot_stride = W;
-            g.slot_sq = (uint64_t)W * W;
-            if ((err = check(launch_leaves(g, n, leaf_.as<uint8_t>() + ((uint64_t)k * W + k) * kSlot, d_err, false,
-                                           false, s),
-                             "leaf hashing")))
-                break;
-        }
-        mark_end(s);
-    } while (false);
-    // join the side stream on every path
-    if (q_used) {
-        if (hipEventRecord(ev_leaves, q) != hipSuccess || hipStreamWaitEvent(s, ev_leaves, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            (void)hipStreamSynchronize(q);
-            if (!err) err = fail(CDA_ERR_DEVICE, "leaf overlap join failed");
-        }
-    }
-    if (err) return err;
-    (void)slots_sq;
-    return enqueue_dah(d_eds, k, n, d_rows, d_cols, d_roots, d_err, d_status, s, true, true);
-}
-
 int Engine::enqueue_extend_dah_serial(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t* d_eds,
                                       uint8_t* d_rows, uint8_t* d_cols, uint8_t* d_roots, uint32_t* d_err,
                                       int32_t* d_status, hipStream_t s) {
-    if (leaf_overlap_ && n <= leaf_overlap_ && !profiling_ && k >= 2)
-        return enqueue_extend_dah_overlap(d_ods, k, n, d_eds, d_rows, d_cols, d_roots, d_err, d_status, s);
     // the first RS launch also sets the push-order words (no separate fill)
     int rc = enqueue_extend(d_ods, k, n, d_eds, s, d_err);
     if (rc) return rc;

@@ -173,8 +173,7 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
     }
     uint32_t out[kSlotWords];
     leaf_node_words(nsw, st.h, out);
-    const size_t slot = g.slot_stride ? sq * g.slot_sq + (size_t)r * g.slot_stride + c : sq * (size_t)g.rows * g.cols + cell;
-    store_slot(slots + slot * kSlot, out);
+    store_slot(slots + (sq * (size_t)g.rows * g.cols + cell) * kSlot, out);
 
     // nmt push-order check of Q0 (fused: this cell's namespace is in nsw)
     if (!parity) {

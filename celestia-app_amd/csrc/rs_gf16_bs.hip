@@ -122,13 +122,11 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
         });
     }
     bs16::sfor<0, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
-#ifdef CDA_BS16_LANEMASK
-    const bs16::LaneMask<0> m{jl};   // A/B: masks derived where used (4 fewer long-lived VGPRs)
-#else
+    // (Masks derived at each use, bs16::LaneMask<0>{jl}: 16 instead of 20
+    // spills, but RS +6-8 % at batch 4; profiles/r05/leaf_overlap_lanemask_ab.txt.)
     uint32_t m[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) m[i] = 0u - ((jl >> i) & 1);
-#endif
     bs16::phase_low_ifft<LOGK>(R, m, w);
 
     // ---- exchanges ------------------------------------------------------------

@@ -107,50 +107,3 @@ def test_hash_split_push_order_status(ctx, bad):
     for i in range(n):
         if i != bad:
             assert bytes(roots[i]) == coracle.extend_dah(ods[i])[3]
-
-
-@pytest.mark.parametrize("k,n", [(1, 1), (2, 3), (16, 2), (128, 1), (128, 4), (512, 1)])
-def test_leaf_overlap_matches_serial(ctx, k, n):
-    """CDA_LEAF_OVERLAP (engine.hip enqueue_extend_dah_overlap): each
-    quadrant's leaves hashed on the context's second stream as soon as the
-    quadrant exists (Q0 beside the first RS launch, read from the packed ODS or
-    from Q0 in place; Q1 and Q2 beside the second).  Same bytes as the serial
-    schedule for the packed and the in-place device entries, the data roots
-    equal the oracle's, and a namespace-order violation in Q0 sets the status
-    of its square only."""
-    import torch
-    ods = np.stack([coracle.random_square(k, 300 + i) for i in range(n)])
-    if k >= 2:
-        sq = ods[n - 1].reshape(k, k, 512)
-        sq[0, 0, :29], sq[0, 1, :29] = sq[0, 1, :29].copy(), sq[0, 0, :29].copy()
-    pc = _ctx_with({"CDA_LEAF_OVERLAP": "16"})
-    W = 2 * k
-    try:
-        outs = {}
-        for name, c in (("serial", ctx), ("overlap", pc)):
-            for inplace in (False, True):
-                d_ods = torch.from_numpy(ods.reshape(-1)).to("cuda")
-                d_eds = torch.zeros((n, W, W, 512), dtype=torch.uint8, device="cuda")
-                d_rows = torch.empty((n, W, 90), dtype=torch.uint8, device="cuda")
-                d_cols = torch.empty_like(d_rows)
-                d_roots = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
-                d_st = torch.empty(n, dtype=torch.int32, device="cuda")
-                if inplace:
-                    d_eds[:, :k, :k] = d_ods.view(n, k, k, 512)
-                    c.extend_dah_inplace_device(k, n, d_eds.data_ptr(), d_rows.data_ptr(), d_cols.data_ptr(),
-                                                d_roots.data_ptr(), d_st.data_ptr())
-                else:
-                    c.extend_dah_device(d_ods.data_ptr(), k, n, d_eds.data_ptr(), d_rows.data_ptr(),
-                                        d_cols.data_ptr(), d_roots.data_ptr(), d_st.data_ptr())
-                torch.cuda.synchronize()
-                outs[(name, inplace)] = [t.cpu().numpy() for t in (d_eds, d_rows, d_cols, d_roots, d_st)]
-        for inplace in (False, True):
-            for a, b in zip(outs[("serial", inplace)], outs[("overlap", inplace)]):
-                assert np.array_equal(a, b), inplace
-        st = outs[("overlap", True)][4]
-        assert [bool(x) for x in st != 0] == [k >= 2 and i == n - 1 and
-                                              bytes(ods[i][0, :29]) != bytes(ods[i][1, :29]) for i in range(n)]
-        if not (k >= 2 and n == 1):   # square 0 is ordered
-            assert bytes(outs[("overlap", False)][3][0]) == coracle.extend_dah(ods[0])[3]
-    finally:
-        pc.close()
