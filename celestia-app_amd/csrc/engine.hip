@@ -1021,15 +1021,19 @@ int Engine::enqueue_parity_d2h(const uint8_t* d_eds, uint32_t k, uint32_t n, uin
                                hipEvent_t ready, hipEvent_t done, int eds_mode, uint8_t* d_par) {
     const size_t W = 2 * (size_t)k, sq_b = W * W * kShare, half = k * W * kShare;
     int rc;
+    const size_t par_b = (size_t)n * 3 * k * k * kShare;
+    if (eds_mode == CDA_EDS_PARITY) {
+        // pack on the compute stream right behind the RS (a few hundred us per
+        // 32 squares, where the compute stream has slack against the copies),
+        // so the copy stream runs nothing but back-to-back linear copies
+        const uint64_t total16 = par_b / 16;
+        hipLaunchKernelGGL(pack_parity_kernel, dim3((uint32_t)((total16 + 255) / 256)), dim3(256), 0, from, d_eds,
+                           d_par, k, total16);
+        if ((rc = check(hipGetLastError(), "pack parity"))) return rc;
+    }
     if ((rc = check(hipEventRecord(ready, from), "hipEventRecord"))) return rc;
     if ((rc = check(hipStreamWaitEvent(copy_out_, ready, 0), "hipStreamWaitEvent"))) return rc;
     if (eds_mode == CDA_EDS_PARITY) {
-        // pack on the copy stream (beside the hashing), then one linear copy
-        const size_t par_b = (size_t)n * 3 * k * k * kShare;
-        const uint64_t total16 = par_b / 16;
-        hipLaunchKernelGGL(pack_parity_kernel, dim3((uint32_t)((total16 + 255) / 256)), dim3(256), 0, copy_out_, d_eds,
-                           d_par, k, total16);
-        if ((rc = check(hipGetLastError(), "pack parity"))) return rc;
         if ((rc = check(hipMemcpyAsync(eds, d_par, par_b, hipMemcpyDeviceToHost, copy_out_), "D2H parity"))) return rc;
         return check(hipEventRecord(done, copy_out_), "hipEventRecord");
     }
