@@ -608,7 +608,11 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     // at config 4's 1024 squares per launch the level tails no longer matter (21 465 split vs 21 528
     // one stream, profiles/r03a/bench_split0.json), and one stream keeps every launch of a kernel the
     // same shape, so per-launch profiler counters divide by a known square count
-    const uint32_t want = hash_split_ >= 0 ? (uint32_t)hash_split_ : (n <= 256 ? 2u : 1u);
+    // k >= 256: one stream -- a k = 512 square's levels already fill the chip
+    // (its subtree launch holds 262 144 lanes), and half-size launches on two
+    // streams ran slower: k = 512 x 4 0.996 -> 0.945 ms per square, x 16
+    // 0.888 -> 0.874 with one stream (profiles/r05/k512_pipeline_hashsplit_ab.txt)
+    const uint32_t want = hash_split_ >= 0 ? (uint32_t)hash_split_ : (n <= 256 && k <= 128 ? 2u : 1u);
     const uint32_t parts = std::min<uint32_t>(std::min<uint32_t>(want, n), kMaxHashParts);
     if (parts > 1 && !profiling_) {
         hipEvent_t go = sync_event(0);
