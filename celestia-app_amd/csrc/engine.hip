@@ -408,14 +408,21 @@ int Engine::run_forests(Forest* f, uint32_t n_forest, uint32_t n_in, uint32_t n,
         uint64_t per_node = 0;   // lanes per subtree root per tree
         for (uint32_t i = 0; i < n_forest; i++) per_node += (uint64_t)n * f[i].n_trees;
         uint32_t sub = stop;
-        // default target: 131072 lanes (two waves per SIMD); 262144 for trees
-        // of >= 1024 leaves (k >= 512: one k = 512 square 1.096 -> 1.087 ms,
-        // 8- instead of 16-leaf subtrees; profiles/r03at/)
-        const uint64_t want = subtree_lanes_ ? subtree_lanes_ : n_in >= 1024 ? 262144u : 131072u;
-        while (sub < n_in && per_node * sub < want) sub *= 2;
+        // default target: 524288 lanes (8 waves per SIMD, 2.67 rounds at the
+        // kernel's 3 waves per SIMD, the shape of config 4's whole-tree launch)
+        // for trees of <= 512 leaves -- config 4's per-GPU shards of 64 / 128
+        // / 256 squares +4-5 % over 131072 lanes on two streams (round 5,
+        // profiles/r05/subtree_lanes_ab.txt); 262144 for trees of >= 1024
+        // leaves (k >= 512: one k = 512 square 1.096 -> 1.087 ms, 8- instead
+        // of 16-leaf subtrees; profiles/r03at/).  Subtrees keep >= 8 leaves
+        // (CDA_SUBTREE); a batch too small to reach the target still takes the
+        // fused launch when it holds 131072 lanes.
+        const uint64_t want = subtree_lanes_ ? subtree_lanes_ : n_in >= 1024 ? 262144u : 524288u;
         // launch_subtrees needs subtrees of >= 4 leaves: a smaller CDA_SUBTREE
         // setting means per-level launches, not a failing launch
-        bool fits = per_node * sub >= want && sub < n_in && n_in / sub >= (uint32_t)std::max(subtree_min_, 4);
+        const uint32_t min_leaves = (uint32_t)std::max(subtree_min_, 4);
+        while (sub < n_in && 2 * (uint64_t)sub * min_leaves <= n_in && per_node * sub < want) sub *= 2;
+        bool fits = per_node * sub >= std::min<uint64_t>(want, 131072) && sub < n_in && n_in / sub >= min_leaves;
         const uint32_t slog = fits ? (uint32_t)__builtin_ctz(n_in / sub) : 0;
         for (uint32_t i = 0; i < n_forest && fits; i++) {
             const uint64_t need = (uint64_t)f[i].n_trees * sub * slog * kSlot;
@@ -612,7 +619,12 @@ int Engine::enqueue_dah(const uint8_t* d_eds, uint32_t k, uint32_t n, uint8_t* d
     // (its subtree launch holds 262 144 lanes), and half-size launches on two
     // streams ran slower: k = 512 x 4 0.996 -> 0.945 ms per square, x 16
     // 0.888 -> 0.874 with one stream (profiles/r05/k512_pipeline_hashsplit_ab.txt)
-    const uint32_t want = hash_split_ >= 0 ? (uint32_t)hash_split_ : (n <= 256 && k <= 128 ? 2u : 1u);
+    // Round 5: one stream from 64 squares up as well -- with the subtree
+    // launch's 524288-lane target (run_forests) one launch fills the chip, and
+    // 64 / 128 / 256 squares ran 4-5 % faster on one stream
+    // (profiles/r05/subtree_lanes_ab.txt); two parts stay for small batches,
+    // whose latency-bound tails the second stream overlaps.
+    const uint32_t want = hash_split_ >= 0 ? (uint32_t)hash_split_ : (n < 64 && k <= 128 ? 2u : 1u);
     const uint32_t parts = std::min<uint32_t>(std::min<uint32_t>(want, n), kMaxHashParts);
     if (parts > 1 && !profiling_) {
         hipEvent_t go = sync_event(0);
