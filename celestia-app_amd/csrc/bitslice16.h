@@ -541,14 +541,17 @@ B16_HD LaneMask<BASE + BY> shifted(const LaneMask<BASE>& m) { return LaneMask<BA
 // One layer over the 8 units: unit distance D, shard bit b, the unit index
 // holding shard bits from SH up (group bits of unit i: (i & ~(2D-1)) << SH),
 // NL masked lane terms (shard bits LB..), NWB uniform wave terms (bits WB..).
+// Only butterflies whose two units lie in [ULO, UHI) (the kernel can run a
+// layer over units 0..3 while units 4..7 are still loading).
 // Per butterfly the shared signals of y are formed once and every term reads
 // them; the wave terms are uniform branches.
 #ifndef CDA_BS16_PAIR_SIGNALS
-template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB, class M>
+template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB, int ULO = 0, int UHI = 8,
+          class M>
 B16_HD void layer8(uint32_t* R, const M& m, uint32_t u) {
     sfor<0, 8, 1>([&](auto ii) {
         constexpr int i = decltype(ii)::value;
-        if constexpr ((i & D) == 0) {
+        if constexpr ((i & D) == 0 && i >= ULO && i + D < UHI) {
             uint32_t* x = R + 16 * i;
             uint32_t* y = R + 16 * (i + D);
             if constexpr (INV) {
@@ -598,11 +601,12 @@ B16_HD void layer8(uint32_t* R, const M& m, uint32_t u) {
     });
 }
 #else
-template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB, class M>
+template <int LOGK, bool INV, int b, int D, int SH, int NL, int LB, int NWB, int WB, int ULO = 0, int UHI = 8,
+          class M>
 B16_HD void layer8(uint32_t* R, const M& m, uint32_t u) {
     sfor<0, 8, 1>([&](auto ii) {
         constexpr int i = decltype(ii)::value;
-        if constexpr ((i & D) == 0) {
+        if constexpr ((i & D) == 0 && i >= ULO && i + D < UHI) {
             uint32_t* x = R + 16 * i;
             uint32_t* y = R + 16 * (i + D);
             if constexpr (INV) {
@@ -632,9 +636,9 @@ B16_HD void layer8(uint32_t* R, const M& m, uint32_t u) {
 }
 #endif
 // LOW layer b (0..2): unit = shard bits 0..2, lane bits 3..6 (m[0..3]), wave bits 7..
-template <int LOGK, bool INV, int b, class M>
+template <int LOGK, bool INV, int b, int ULO = 0, int UHI = 8, class M>
 B16_HD void low_layer(uint32_t* R, const M& m, uint32_t u) {
-    layer8<LOGK, INV, b, 1 << b, 0, 4, 3, LOGK - 7, 7>(R, m, u);
+    layer8<LOGK, INV, b, 1 << b, 0, 4, 3, LOGK - 7, 7, ULO, UHI>(R, m, u);
 }
 // M1 layer b (3..5): unit = shard bits 3..5, lane bit 6 (m[3]), wave bits 7..
 template <int LOGK, bool INV, int b, class M>

@@ -121,13 +121,26 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
                 p[q] = u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2], R[16 * u + 4 * q + 3]};
         });
     }
-    bs16::sfor<0, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
     // (Masks derived at each use, bs16::LaneMask<0>{jl}: 16 instead of 20
     // spills, but RS +6-8 % at batch 4; profiles/r05/leaf_overlap_lanemask_ab.txt.)
     uint32_t m[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) m[i] = 0u - ((jl >> i) & 1);
+#ifndef CDA_BS16_NO_SPLIT
+    // LOW IFFT layers 0 and 1 pair units within 0..3 and within 4..7: run them
+    // on units 0..3 while the loads of units 4..7 are still in flight (the
+    // wait for a unit's data sits before its planes transform).
+    bs16::sfor<0, 4, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
+    bs16::low_layer<LOGK, true, 0, 0, 4>(R, m, w);
+    bs16::low_layer<LOGK, true, 1, 0, 4>(R, m, w);
+    bs16::sfor<4, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
+    bs16::low_layer<LOGK, true, 0, 4, 8>(R, m, w);
+    bs16::low_layer<LOGK, true, 1, 4, 8>(R, m, w);
+    bs16::low_layer<LOGK, true, 2>(R, m, w);
+#else
+    bs16::sfor<0, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
     bs16::phase_low_ifft<LOGK>(R, m, w);
+#endif
 
     // ---- exchanges ------------------------------------------------------------
     // X12 / X21 (LOW <-> M1, within each wave): unit u of lane (b4, jl) <->
@@ -192,9 +205,8 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     x23(false);
     bs16::phase_m1_fft<LOGK>(R, m, w);
     x12(true);
-    bs16::phase_low_fft<LOGK>(R, m, w);
-    // ---- planes -> bytes, store parity -----------------------------------------
-    bs16::sfor<0, 8, 1>([&](auto uu) {
+    // ---- LOW FFT, planes -> bytes, store parity --------------------------------
+    auto store = [&](auto uu) {
         constexpr int u = decltype(uu)::value;
         bs16::block_planes(R + 16 * u);
         uint32_t o = d0 + u * g.dst_sh;
@@ -203,7 +215,20 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int q = 0; q < 4; q++)
             p[q] = u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2], R[16 * u + 4 * q + 3]};
-    });
+    };
+#ifndef CDA_BS16_NO_SPLIT
+    // mirror of the entry: units 0..3 finish and store while 4..7 compute
+    bs16::low_layer<LOGK, false, 2>(R, m, w);
+    bs16::low_layer<LOGK, false, 1, 0, 4>(R, m, w);
+    bs16::low_layer<LOGK, false, 0, 0, 4>(R, m, w);
+    bs16::sfor<0, 4, 1>(store);
+    bs16::low_layer<LOGK, false, 1, 4, 8>(R, m, w);
+    bs16::low_layer<LOGK, false, 0, 4, 8>(R, m, w);
+    bs16::sfor<4, 8, 1>(store);
+#else
+    bs16::phase_low_fft<LOGK>(R, m, w);
+    bs16::sfor<0, 8, 1>(store);
+#endif
 }
 
 template <int LOGK>
