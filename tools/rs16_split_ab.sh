@@ -1,8 +1,10 @@
 #!/bin/bash
 # GPU-box A/B of the k = 512 encoder's LOW-layer split (round 5): the product
-# kernel runs LOW IFFT layers 0-1 on units 0..3 while units 4..7 still load and
-# stores units 0..3 while 4..7 compute; build_var/nosplit/libcda.so is the same
-# source built with -DCDA_BS16_NO_SPLIT.  Parity of the product build first
+# kernel runs LOW IFFT layer 0 on each pair of units and layer 1 on each quad
+# as soon as their loads land, and stores each pair of units as soon as LOW
+# FFT is done with it; build_var/split2/libcda.so (-DCDA_BS16_SPLIT2) splits
+# only into halves, build_var/nosplit/libcda.so (-DCDA_BS16_NO_SPLIT) not at
+# all.  Then a kernel trace of the timed region of each (TRACE=1).  Parity of the product build first
 # (every k = 512 / GF(2^16) GPU test), then interleaved bench runs at batch
 # 1 / 4 / 16.  Output: gpurun_out/<tag>/.
 set -o pipefail
@@ -13,11 +15,11 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
   -k "512 or gf16 or codec or split or linear or repair" > "$OUT/parity.log" 2>&1 || exit $?
 tail -1 "$OUT/parity.log"
 for rep in 1 2; do
-  for v in split nosplit; do
+  for v in ${VARIANTS:-split split2 nosplit}; do
     for b in 1 4 16; do
       case $v in
         split) E="" ;;
-        nosplit) E="CDA_LIB=$PWD/celestia-app_amd/build_var/nosplit/libcda.so" ;;
+        *) E="CDA_LIB=$PWD/celestia-app_amd/build_var/$v/libcda.so" ;;
       esac
       env $E timeout -k 10 200 python -u bench.py --k 512 --batch $b --no-cpu --no-extras --steps 20 \
         > "$OUT/ab_${v}_b${b}_r${rep}.log" 2>&1 || exit $?
@@ -33,4 +35,12 @@ print(sys.argv[2], "batch", b, "ms/sq %.4f" % (j["ms_per_step"] / b), "RS/sq %.4
 PY
     done
   done
+done
+[ "${TRACE:-0}" = 1 ] || exit 0
+cd /tmp && export TMPDIR=/tmp
+for v in split nosplit; do
+  L=""; [ $v = split ] || L="$GRAFT_REPO_ROOT/celestia-app_amd/build_var/$v/libcda.so"
+  CDA_LIB=${L:-$GRAFT_REPO_ROOT/celestia-app_amd/libcda.so} timeout -k 10 200 rocprofv3 --kernel-trace --stats \
+    -d "$GRAFT_REPO_ROOT/$OUT/trace_$v" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --k 512 --batch 1 --no-cpu \
+    --no-extras --steps 40 > "$GRAFT_REPO_ROOT/$OUT/trace_$v.log" 2>&1 || exit $?
 done
