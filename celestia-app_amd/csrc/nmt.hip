@@ -104,9 +104,38 @@ __device__ __forceinline__ void load_raw16(const uint4* p, uint32_t (&w)[16]) {
 // Big-endian message word from share bytes 4j+2 .. 4j+5 (raw words j, j+1).
 __device__ __forceinline__ uint32_t body_word(uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x02030405u); }
 
+// Push-order check of a Q0 cell against its right / lower neighbour (fused
+// into the leaf launch: this cell's namespace is in nsw).
+__device__ __forceinline__ void leaf_order_check(const CellGrid& g, const uint8_t* cellp, const uint32_t (&nsw)[8],
+                                                 uint32_t* err, int check_rows, int check_cols, uint32_t r, uint32_t c,
+                                                 uint32_t gr, uint32_t gc) {
+    const uint32_t k = g.k;
+    uint32_t nb[8];
+    uint32_t key = 0xFFFFFFFFu;
+    if (check_rows && gc + 1 < k && c + 1 < g.cols) {
+        load_ns_be(cellp + SH, nb);
+        if (ns_less(nb, nsw)) key = min(key, (0u << 24) | (gr << 12) | (gc + 1));
+    }
+    if (check_cols && gr + 1 < k && r + 1 < g.rows) {
+        load_ns_be(cellp + (size_t)g.row_stride * SH, nb);
+        if (ns_less(nb, nsw)) key = min(key, (1u << 24) | (gc << 12) | (gr + 1));
+    }
+    if (key != 0xFFFFFFFFu) atomicMin(err, key);
+}
+
 // One virtual block (bx = 256-cell group, by = square) of the leaf launch.
+// ns_lds: this thread's 8 namespace words between the first chunk and the
+// leaf node (Q0 cells).  Round 5: the namespace used to be reloaded from
+// global memory after the ninth block and the neighbours' namespaces read
+// there too -- lines long evicted by then, ~1.2x the algorithmic bytes at the
+// fabric (r04s / r05m PMC); now the check runs while the neighbours' first
+// chunks are in flight in the same wave / the next workgroup, and the own
+// namespace waits in LDS: the launch's FETCH_SIZE -5 %, WRITE_SIZE -20 % (its
+// six spilled values gone, 128 -> 125 VGPRs), time equal (VALU-bound;
+// profiles/r05/leaf_ns_ab.txt).
 __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restrict__ slots, uint32_t* __restrict__ err,
-                                           int check_rows, int check_cols, uint32_t bx, uint32_t by) {
+                                           int check_rows, int check_cols, uint32_t bx, uint32_t by,
+                                           uint32_t (*ns_lds)[8]) {
     const uint32_t cell = bx * 256 + threadIdx.x;
     if (cell >= g.rows * g.cols) return;
     const size_t sq = by;
@@ -121,6 +150,16 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
     sha_init(st);
     uint32_t cur[16], tail[8], w[16];
     load_raw16(src, cur);
+    if (!parity) {
+        uint32_t nsw[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) nsw[i] = bswap32(cur[i]);
+        nsw[7] &= 0xFF000000u;
+        uint4* o = reinterpret_cast<uint4*>(ns_lds[threadIdx.x]);
+        o[0] = make_uint4(nsw[0], nsw[1], nsw[2], nsw[3]);
+        o[1] = make_uint4(nsw[4], nsw[5], nsw[6], nsw[7]);
+        leaf_order_check(g, cellp, nsw, err + sq, check_rows, check_cols, r, c, gr, gc);
+    }
     uint32_t nxt[16];   // the next 64-B chunk in flight during each block
     load_raw16(src + 4, nxt);
     // block 0: 0x00 || ns(29) || share[0:34]; a parity leaf's first 7 words
@@ -163,32 +202,20 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
     w[15] = kLeafMsgBits;
     sha_compress(st, w);
 
-    // namespace (big-endian words) reloaded: L2/MALL-hot, saves 8 live VGPRs
+    // namespace (big-endian words): saved in LDS, 8 VGPRs not live here
     uint32_t nsw[8];
     if (parity) {
 #pragma unroll
         for (int i = 0; i < 8; i++) nsw[i] = 0xFFFFFFFFu;
     } else {
-        load_ns_be(cellp, nsw);
+        const uint4* q = reinterpret_cast<const uint4*>(ns_lds[threadIdx.x]);
+        const uint4 a = q[0], b = q[1];
+        nsw[0] = a.x; nsw[1] = a.y; nsw[2] = a.z; nsw[3] = a.w;
+        nsw[4] = b.x; nsw[5] = b.y; nsw[6] = b.z; nsw[7] = b.w;
     }
     uint32_t out[kSlotWords];
     leaf_node_words(nsw, st.h, out);
     store_slot(slots + (sq * (size_t)g.rows * g.cols + cell) * kSlot, out);
-
-    // nmt push-order check of Q0 (fused: this cell's namespace is in nsw)
-    if (!parity) {
-        uint32_t nb[8];
-        uint32_t key = 0xFFFFFFFFu;
-        if (check_rows && gc + 1 < k && c + 1 < g.cols) {
-            load_ns_be(cellp + SH, nb);
-            if (ns_less(nb, nsw)) key = min(key, (0u << 24) | (gr << 12) | (gc + 1));
-        }
-        if (check_cols && gr + 1 < k && r + 1 < g.rows) {
-            load_ns_be(cellp + (size_t)g.row_stride * SH, nb);
-            if (ns_less(nb, nsw)) key = min(key, (1u << 24) | (gc << 12) | (gr + 1));
-        }
-        if (key != 0xFFFFFFFFu) atomicMin(err + sq, key);
-    }
 }
 
 // The hash launches run a 1-D grid over virtual blocks b = by * nbx + bx: one
@@ -199,8 +226,9 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDA_LEAF_WAVES))) void leaf_kernel(
     const CellGrid g, uint8_t* __restrict__ slots, uint32_t* __restrict__ err, int check_rows, int check_cols,
     uint32_t nbx, uint32_t nblocks) {
+    __shared__ __attribute__((aligned(16))) uint32_t ns_lds[256][8];
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
-        leaf_block(g, slots, err, check_rows, check_cols, b % nbx, b / nbx);
+        leaf_block(g, slots, err, check_rows, check_cols, b % nbx, b / nbx, ns_lds);
 }
 
 // ---------------------------------------------------------------------------
