@@ -668,8 +668,21 @@ int cda_split_offsets(uint32_t k, uint32_t world, int what, uint32_t n, const ui
     if (!world || !off || (n && !a)) return CDA_ERR_INVALID;
     const cda::SplitLayout L(k, world);
     if (!L.valid()) return CDA_ERR_INVALID;
+    // (a, b) ranges per kind; b must be given where the kind reads it
+    uint32_t amax, bmax = 1;
+    switch (what) {
+        case CDA_SPLIT_SEND: amax = L.R; bmax = L.W; break;
+        case CDA_SPLIT_BLOCK: amax = L.W; bmax = L.C; break;
+        case CDA_SPLIT_COMBINE: amax = L.G; bmax = L.W; break;
+        case CDA_SPLIT_SEND_PIECE: case CDA_SPLIT_RECV_PIECE: case CDA_SPLIT_GATHER_SUB: case CDA_SPLIT_GATHER_COL:
+            amax = L.G; break;
+        default: return CDA_ERR_INVALID;
+    }
+    if (n && bmax > 1 && !b) return CDA_ERR_INVALID;
+    for (uint32_t i = 0; i < n; i++)
+        if (a[i] >= amax || (bmax > 1 && b[i] >= bmax)) return CDA_ERR_INVALID;
     for (uint32_t i = 0; i < n; i++) {
-        const uint32_t x = a[i], y = b ? b[i] : 0;
+        const uint32_t x = a[i], y = bmax > 1 ? b[i] : 0;
         switch (what) {
             case CDA_SPLIT_SEND: off[i] = L.send_off(x, y); break;
             case CDA_SPLIT_SEND_PIECE: off[i] = L.send_piece_off(x); break;

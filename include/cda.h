@@ -281,7 +281,9 @@ int cda_split_layout(uint32_t k, uint32_t world, cda_split_layout_t *out);
  *   CDA_SPLIT_BLOCK       column-block byte offset of EDS row a, local column b
  *   CDA_SPLIT_GATHER_SUB  slot-area byte offset of rank a's W row subtrees (rank 0)
  *   CDA_SPLIT_GATHER_COL  slot-area byte offset of rank a's C column roots (rank 0)
- *   CDA_SPLIT_COMBINE     slot index, in the gathered subtrees, of rank a's node of row b */
+ *   CDA_SPLIT_COMBINE     slot index, in the gathered subtrees, of rank a's node of row b
+ * CDA_ERR_INVALID (nothing written) for an unknown kind, an index out of its
+ * range (r < R, col < W, row < W, c < C, ranks < world) or b NULL where read. */
 #define CDA_SPLIT_SEND 0
 #define CDA_SPLIT_SEND_PIECE 1
 #define CDA_SPLIT_RECV_PIECE 2

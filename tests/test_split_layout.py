@@ -139,3 +139,20 @@ def test_split_layout_sizes():
     assert L["piece_bytes"] == 64 * 128 * SH == 4 << 20            # 4 MiB per rank pair
     assert L["send_bytes"] == 8 * L["piece_bytes"] == 32 << 20     # 32 MiB send, 64 MiB column block
     assert L["col_block_bytes"] == 1024 * 128 * SH == 64 << 20
+
+
+def test_split_offsets_reject_out_of_range():
+    k, G = 16, 4                       # R = 4, C = 8, W = 32
+    ok = _lib.split_offsets(k, G, _lib.CDA_SPLIT_SEND, [3], [31])
+    assert ok[0] == ((3 * 4 + 3) * 8 + 7) * SH          # col 31: piece 3, local column 7
+    for what, a, b in ((_lib.CDA_SPLIT_SEND, [4], [0]),            # r >= R
+                       (_lib.CDA_SPLIT_SEND, [0], [32]),           # col >= W
+                       (_lib.CDA_SPLIT_SEND, [0], None),           # b needed
+                       (_lib.CDA_SPLIT_BLOCK, [32], [0]),          # row >= W
+                       (_lib.CDA_SPLIT_BLOCK, [0], [8]),           # c >= C
+                       (_lib.CDA_SPLIT_COMBINE, [4], [0]),         # rank >= G
+                       (_lib.CDA_SPLIT_SEND_PIECE, [4], None),
+                       (_lib.CDA_SPLIT_GATHER_COL, [7], None),
+                       (99, [0], [0])):                            # unknown kind
+        with pytest.raises(_lib.CdaError):
+            _lib.split_offsets(k, G, what, a, b)
