@@ -90,9 +90,9 @@ __global__ __launch_bounds__(256) void row_order_kernel(const CellGrid g, uint32
 // 0x00 || ns || share.  The share is streamed in 64-B chunks of raw
 // little-endian words; every big-endian message word is ONE v_perm_b32 of two
 // raw words (byte swap and the 30-byte message offset folded together).  Only
-// the upper half of the previous chunk (8 words) is carried between blocks, so
-// the kernel stays under 96 VGPRs (5+ waves per SIMD to hide the dependent
-// SHA round chain).
+// the upper half of the previous chunk (8 words) is carried between blocks.
+// 125 VGPRs, four waves per SIMD (CDA_LEAF_WAVES); at five the compiler fits
+// 96 VGPRs only by spilling 34 values.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void load_raw16(const uint4* p, uint32_t (&w)[16]) {
 #pragma unroll
