@@ -108,6 +108,50 @@ def test_push_order_error(ctx):
     assert np.array_equal(eds.array().reshape(-1, 512), coracle.extend(ods.reshape(-1, 512)))
 
 
+def _first_violation(ods):
+    """Brute-force nmt push-order check of the Q0 rows and columns: the
+    smallest (axis, index, position) whose namespace is below its
+    predecessor's (rows before columns), as cda_push_order_detail reports."""
+    k = ods.shape[0]
+    ns = [[bytes(ods[r, c, :29]) for c in range(k)] for r in range(k)]
+    bad = [(0, r, c) for r in range(k) for c in range(1, k) if ns[r][c] < ns[r][c - 1]]
+    bad += [(1, c, r) for c in range(k) for r in range(1, k) if ns[r][c] < ns[r - 1][c]]
+    return min(bad) if bad else None
+
+
+@pytest.mark.parametrize("case", ["row_last_pair", "col_last_row", "row_first_pair", "row_and_col", "last_col"])
+def test_push_order_edges(ctx, case):
+    """Round 5 moved the Q0 push-order check to the leaf kernel's first chunk:
+    violations at the square's edges (first / last Q0 row and column, the
+    boundary to the parity half) and several at once report the same first
+    violation as a brute-force check, and the EDS is unchanged."""
+    k = 16
+    ods = coracle.random_square(k, 31).reshape(k, k, 512).copy()
+
+    def swap(a, b):
+        ods[a][:29], ods[b][:29] = ods[b][:29].copy(), ods[a][:29].copy()
+
+    if case == "row_last_pair":
+        swap((k - 1, k - 2), (k - 1, k - 1))
+    elif case == "col_last_row":
+        ods[k - 1, 0, :29] = ods[0, 0, :29]          # below its upper neighbour only
+    elif case == "row_first_pair":
+        swap((0, 0), (0, 1))
+    elif case == "row_and_col":
+        ods[k - 1, 0, :29] = ods[0, 0, :29]
+        swap((5, 9), (5, 10))
+    else:
+        ods[1, k - 1, :29] = ods[0, 0, :29]          # last Q0 column, row 1
+    want = _first_violation(ods)
+    if want is None:
+        pytest.skip("perturbation left the square ordered (equal namespaces)")
+    eds = da.extend_shares(ods.reshape(-1, 512))
+    with pytest.raises(PushOrderError):
+        da.new_data_availability_header(eds)
+    assert ctx.push_order_detail() == want
+    assert np.array_equal(eds.array().reshape(-1, 512), coracle.extend(ods.reshape(-1, 512)))
+
+
 def test_block408_on_gpu(ctx):
     """Mainnet block 408 (k=32): GPU data root == header.data_hash."""
     import gzip, json, os
