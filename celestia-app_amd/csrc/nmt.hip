@@ -218,6 +218,89 @@ __device__ __forceinline__ void leaf_block(const CellGrid& g, uint8_t* __restric
     store_slot(slots + (sq * (size_t)g.rows * g.cols + cell) * kSlot, out);
 }
 
+// Lane-pair leaves (round 5), for leaf launches of at most half a wave per
+// SIMD of cells (k <= 64 squares): two lanes per cell run one instruction
+// stream (sha_pair_compress: 1 040 instead of ~1 430 instructions per
+// compression on the chain), so twice the SIMDs hold a wave.  One k = 64
+// square 0.155 -> 0.150 ms (leaves 31 -> 28 us); at one k = 128 square (one
+// wave per SIMD either way) the two pair waves per SIMD share its issue and
+// the leaves take 34 -> 42 us, so 65 536-cell launches stay one lane per
+// cell (profiles/r05/leaf_pair_ab.txt).  Both
+// lanes of a pair load the same bytes and build the same message words; the
+// e-side lane stores the slot and runs the push-order check.  No parity
+// mid-state (block 0 of a parity leaf runs all 64 rounds).  128 cells per
+// 256-thread workgroup.
+__global__ __launch_bounds__(256) void leaf_pair_kernel(const CellGrid g, uint8_t* __restrict__ slots,
+                                                        uint32_t* __restrict__ err, int check_rows, int check_cols,
+                                                        uint32_t nbx) {
+    const uint32_t bx = blockIdx.x % nbx, by = blockIdx.x / nbx;
+    const uint32_t cell = bx * 128 + (threadIdx.x >> 1);
+    if (cell >= g.rows * g.cols) return;   // both lanes of a pair leave together
+    const bool A = threadIdx.x & 1;
+    const size_t sq = by;
+    const uint32_t r = cell / g.cols, c = cell % g.cols;
+    const uint32_t gr = g.row0 + r, gc = g.col0 + c, k = g.k;
+    const bool parity = !(gr < k && gc < k);
+    const uint8_t* cellp = g.base + sq * g.sq + ((size_t)r * g.row_stride + c) * SH;
+    const uint4* src = reinterpret_cast<const uint4*>(cellp);
+
+    Sha<true> h;
+    h.init(A);
+    uint32_t cur[16], tail[8], w[16], nsw[8];
+    load_raw16(src, cur);
+    if (parity) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nsw[i] = 0xFFFFFFFFu;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nsw[i] = bswap32(cur[i]);
+        nsw[7] &= 0xFF000000u;
+        if (!A) leaf_order_check(g, cellp, nsw, err + sq, check_rows, check_cols, r, c, gr, gc);
+    }
+    uint32_t nxt[16];
+    load_raw16(src + 4, nxt);
+#pragma unroll
+    for (int i = 8; i < 16; i++) w[i] = body_word(cur[i - 8], cur[i - 7]);
+    if (parity) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) w[i] = kLeafParityHead[i];
+        w[7] = __builtin_amdgcn_perm(cur[0], cur[0], 0x0D0D0001u);
+    } else {
+        w[0] = __builtin_amdgcn_perm(cur[0], cur[0], 0x0C000102u);
+#pragma unroll
+        for (int i = 1; i < 7; i++) w[i] = __builtin_amdgcn_perm(cur[i], cur[i - 1], 0x03040506u);
+        w[7] = __builtin_amdgcn_perm(cur[7], cur[6], 0x03040C0Cu) | __builtin_amdgcn_perm(cur[0], cur[0], 0x0C0C0001u);
+    }
+    h.compress(w, A);
+#pragma unroll
+    for (int i = 0; i < 8; i++) tail[i] = cur[8 + i];
+#pragma unroll 1
+    for (int b = 1; b < 8; b++) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+        if (b < 7) load_raw16(src + 4 * (b + 1), nxt);
+#pragma unroll
+        for (int t = 0; t < 7; t++) w[t] = body_word(tail[t], tail[t + 1]);
+        w[7] = body_word(tail[7], cur[0]);
+#pragma unroll
+        for (int t = 8; t < 16; t++) w[t] = body_word(cur[t - 8], cur[t - 7]);
+#pragma unroll
+        for (int i = 0; i < 8; i++) tail[i] = cur[8 + i];
+        h.compress(w, A);
+    }
+#pragma unroll
+    for (int t = 0; t < 7; t++) w[t] = body_word(tail[t], tail[t + 1]);
+    w[7] = __builtin_amdgcn_perm(tail[7], tail[7], 0x02030C0Cu) | 0x8000u;
+#pragma unroll
+    for (int t = 8; t < 15; t++) w[t] = 0;
+    w[15] = kLeafMsgBits;
+    h.compress(w, A);
+    uint32_t D[8], out[kSlotWords];
+    h.digest(A, D);
+    leaf_node_words(nsw, D, out);
+    if (!A) store_slot(slots + (sq * (size_t)g.rows * g.cols + cell) * kSlot, out);
+}
+
 // The hash launches run a 1-D grid over virtual blocks b = by * nbx + bx: one
 // block per workgroup when the grid covers them all, or a capped persistent
 // grid (CDA_HASH_WG_PER_CU workgroups per CU) whose workgroups stride over
@@ -981,8 +1064,25 @@ static uint32_t hash_grid(uint32_t nblocks) {
     return cap && nblocks > cap ? cap : nblocks;
 }
 
+// CDA_LEAF_PAIR_MAX: cells per launch up to which the lane-pair leaf kernel
+// runs (default 32 768 = half a wave per SIMD of one-lane cells; 0 = never).
+static uint64_t leaf_pair_max() {
+    static const uint64_t v = [] {
+        const char* e = getenv("CDA_LEAF_PAIR_MAX");
+        return e ? strtoull(e, nullptr, 10) : 32768ull;
+    }();
+    return v;
+}
+
 hipError_t launch_leaves(const CellGrid& g, uint32_t n, uint8_t* slots, uint32_t* err, bool check_rows,
                          bool check_cols, hipStream_t s) {
+    const uint64_t cells = (uint64_t)g.rows * g.cols * n;
+    if (cells > 0 && cells <= leaf_pair_max() && pair_sha_enabled()) {
+        const uint32_t nbx2 = (g.rows * g.cols + 127) / 128;
+        hipLaunchKernelGGL(leaf_pair_kernel, dim3(nbx2 * n), dim3(256), 0, s, g, slots, err, check_rows ? 1 : 0,
+                           check_cols ? 1 : 0, nbx2);
+        return hipGetLastError();
+    }
     const uint32_t nbx = (g.rows * g.cols + 255) / 256, nblocks = nbx * n;
     if (nblocks == 0) return hipSuccess;
     hipLaunchKernelGGL(leaf_kernel, dim3(hash_grid(nblocks)), dim3(256),
