@@ -72,7 +72,27 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     constexpr int K = 1 << LOGK;
     rs_err_init(job);
     extern __shared__ u32x4 X[];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, b4 = lane & 3, jl = lane >> 2;
+    const uint32_t tid = threadIdx.x;
+    // Lane-derived values are recomputed from tid once per exchange call and
+    // per butterfly phase (the empty asm keeps the compiler from carrying them
+    // across the phases, where it spilled them): k = 512 13 -> 0 spilled
+    // values, 889 -> 814 MB per square at the fabric, RS equal at batch 1 and
+    // -5 % at batch 16 (profiles/r05/rs16_spill_ab.txt; recomputing at every
+    // use cost +14 % VALU instructions).
+    struct LaneIds {
+        uint32_t lane, b4, jl;
+    };
+    auto ids = [&]() {
+        uint32_t t = tid;
+        asm volatile("" : "+v"(t));
+        const uint32_t l = t & 63;
+        return LaneIds{l, l & 3, l >> 2};
+    };
+    auto lane_masks = [&](uint32_t (&m)[4]) {
+        const uint32_t jl = ids().jl;
+#pragma unroll
+        for (int i = 0; i < 4; i++) m[i] = 0u - ((jl >> i) & 1);
+    };
     // The wave -> shard-bit mapping is rotated per workgroup: the wave with
     // wave bits 11 runs both uniform-branch terms of every LOW / M1 butterfly,
     // the one with 00 none, and the waves of a workgroup go to the SIMDs of a
@@ -89,10 +109,9 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     uint8_t* E = job.dst + (size_t)blockIdx.y * job.dst_sq;
     // LOW layout: unit u of lane (b4, jl) of wave w is shard w << 7 | jl << 3 | u,
     // block 4 half + b4: uniform part (w, u) in SGPRs + a per-lane offset
-    const uint32_t blk_off = 64 * (4 * half + b4);
     const uint32_t s0 = g.src_off + c * g.src_cw + (w << 7) * g.src_sh;
     const uint32_t d0 = g.dst_off + c * g.dst_cw + (w << 7) * g.dst_sh;
-    const uint32_t ls = blk_off + 8 * jl * g.src_sh, ld = blk_off + 8 * jl * g.dst_sh;
+    const uint32_t ls = 64 * (4 * half + ids().b4) + 8 * ids().jl * g.src_sh;
     uint32_t R[128];
     // ---- load + planes + LOW IFFT --------------------------------------------
     bs16::sfor<0, 8, 1>([&](auto uu) {
@@ -110,7 +129,8 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
         }
     });
     if (g.cpy_off != kNoCopy) {   // the ODS copy into Q0 (packed entry)
-        const uint32_t c0 = g.cpy_off + c * g.cpy_cw + (w << 7) * g.cpy_sh, lc = blk_off + 8 * jl * g.cpy_sh;
+        const uint32_t c0 = g.cpy_off + c * g.cpy_cw + (w << 7) * g.cpy_sh;
+        const uint32_t lc = 64 * (4 * half + ids().b4) + 8 * ids().jl * g.cpy_sh;
         bs16::sfor<0, 8, 1>([&](auto uu) {
             constexpr int u = decltype(uu)::value;
             uint32_t o = c0 + u * g.cpy_sh;
@@ -124,8 +144,7 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     // (Masks derived at each use, bs16::LaneMask<0>{jl}: 16 instead of 20
     // spills, but RS +6-8 % at batch 4; profiles/r05/leaf_overlap_lanemask_ab.txt.)
     uint32_t m[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) m[i] = 0u - ((jl >> i) & 1);
+    lane_masks(m);
 #if defined(CDA_BS16_SPLIT2)
     // LOW IFFT layers 0 and 1 pair units within 0..3 and within 4..7: run them
     // on units 0..3 while the loads of units 4..7 are still in flight (the
@@ -166,12 +185,13 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     // dst unit) * 64 + (dst lane ^ (dst unit & 1) << 2): the XOR keeps the two
     // jl of an 8-lane group on distinct bank groups for writer and reader.
     auto x12 = [&](bool barrier) {
+        const LaneIds I = ids();
         if (barrier) __syncthreads();   // the buffer's previous readers (other waves) are done
         bs16::sfor<0, 4 / kChunksPerRound, 1>([&](auto rr) {
             constexpr int rnd = decltype(rr)::value;
             bs16::sfor<0, 8, 1>([&](auto uu) {
                 constexpr int u = decltype(uu)::value;
-                const uint32_t du = jl & 7, dl = (b4 | ((jl & 8) | u) << 2) ^ ((du & 1) << 2);
+                const uint32_t du = I.jl & 7, dl = (I.b4 | ((I.jl & 8) | u) << 2) ^ ((du & 1) << 2);
                 bs16::sfor<0, kChunksPerRound, 1>([&](auto cc) {
                     constexpr int cq = decltype(cc)::value, q = rnd * kChunksPerRound + cq;
                     lds_st(X, ((cq * NW + w) * 8 + du) * 64 + dl, R + 16 * u + 4 * q);
@@ -182,7 +202,7 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
                 constexpr int u = decltype(uu)::value;
                 bs16::sfor<0, kChunksPerRound, 1>([&](auto cc) {
                     constexpr int cq = decltype(cc)::value, q = rnd * kChunksPerRound + cq;
-                    lds_ld(X, ((cq * NW + w) * 8 + u) * 64 + (lane ^ ((u & 1) << 2)), R + 16 * u + 4 * q);
+                    lds_ld(X, ((cq * NW + w) * 8 + u) * 64 + (I.lane ^ ((u & 1) << 2)), R + 16 * u + 4 * q);
                 });
             });
         });
@@ -190,46 +210,51 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     // X23 / X32 (M1 <-> M2, all waves): slot (chunk * K + shard) * 4 + b4.
     //   M1 (w, jl, u): shard w << 7 | (jl >> 3) << 6 | u << 3 | jl & 7
     //   M2 (w, jl, u): shard u << (LOGK - 3) | w << 4 | jl
-    auto m1_shard = [&](uint32_t u) { return w << 7 | (jl >> 3) << 6 | u << 3 | (jl & 7); };
-    auto m2_shard = [&](uint32_t u) { return u << (LOGK - 3) | w << 4 | jl; };
+    auto m1_shard = [&](uint32_t u, uint32_t jl) { return w << 7 | (jl >> 3) << 6 | u << 3 | (jl & 7); };
+    auto m2_shard = [&](uint32_t u, uint32_t jl) { return u << (LOGK - 3) | w << 4 | jl; };
     auto x23 = [&](bool to_m2) {
+        const LaneIds I = ids();
         bs16::sfor<0, 4 / kChunksPerRound, 1>([&](auto rr) {
             constexpr int rnd = decltype(rr)::value;
             __syncthreads();
             bs16::sfor<0, 8, 1>([&](auto uu) {
                 constexpr int u = decltype(uu)::value;
-                const uint32_t sh = to_m2 ? m1_shard(u) : m2_shard(u);
+                const uint32_t sh = to_m2 ? m1_shard(u, I.jl) : m2_shard(u, I.jl);
                 bs16::sfor<0, kChunksPerRound, 1>([&](auto cc) {
                     constexpr int cq = decltype(cc)::value;
-                    lds_st(X, (cq * K + sh) * 4 + b4, R + 16 * u + 4 * (rnd * kChunksPerRound + cq));
+                    lds_st(X, (cq * K + sh) * 4 + I.b4, R + 16 * u + 4 * (rnd * kChunksPerRound + cq));
                 });
             });
             __syncthreads();
             bs16::sfor<0, 8, 1>([&](auto uu) {
                 constexpr int u = decltype(uu)::value;
-                const uint32_t sh = to_m2 ? m2_shard(u) : m1_shard(u);
+                const uint32_t sh = to_m2 ? m2_shard(u, I.jl) : m1_shard(u, I.jl);
                 bs16::sfor<0, kChunksPerRound, 1>([&](auto cc) {
                     constexpr int cq = decltype(cc)::value;
-                    lds_ld(X, (cq * K + sh) * 4 + b4, R + 16 * u + 4 * (rnd * kChunksPerRound + cq));
+                    lds_ld(X, (cq * K + sh) * 4 + I.b4, R + 16 * u + 4 * (rnd * kChunksPerRound + cq));
                 });
             });
         });
     };
 
     x12(false);   // the first exchange: the workgroup's LDS is untouched so far
+    lane_masks(m);
     bs16::phase_m1_ifft<LOGK>(R, m, w);
     x23(true);
     bs16::phase_m2<LOGK>(R);
     x23(false);
+    lane_masks(m);
     bs16::phase_m1_fft<LOGK>(R, m, w);
     x12(true);
+    lane_masks(m);
     // ---- LOW FFT, planes -> bytes, store parity --------------------------------
     auto store = [&](auto uu) {
         constexpr int u = decltype(uu)::value;
         bs16::block_planes(R + 16 * u);
         uint32_t o = d0 + u * g.dst_sh;
         asm volatile("" : "+s"(o));
-        u32x4* p = reinterpret_cast<u32x4*>(E + o + ld);
+        const LaneIds I = ids();
+        u32x4* p = reinterpret_cast<u32x4*>(E + o + 64 * (4 * half + I.b4) + 8 * I.jl * g.dst_sh);
 #pragma unroll
         for (int q = 0; q < 4; q++)
             p[q] = u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2], R[16 * u + 4 * q + 3]};
