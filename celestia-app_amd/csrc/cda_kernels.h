@@ -32,6 +32,10 @@ struct RsJob {
     // (the push-order words of the hashing that follows, set by the RS launch
     // instead of a separate fill)
     uint32_t* err_init = nullptr;
+    // GF(2^16) bitsliced encoder: raise the wave priority (s_setprio) while a
+    // workgroup loads and while it stores (Engine::enqueue_extend, batches of
+    // <= CDA_RS16_PRIO_MAX squares)
+    uint32_t prio = 0;
 };
 #if defined(__HIPCC__)
 __device__ __forceinline__ void rs_err_init(const RsJob& job) {

@@ -71,6 +71,13 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     constexpr int NW = 1 << (LOGK - 7);    // waves per workgroup
     constexpr int K = 1 << LOGK;
     rs_err_init(job);
+    // Wave priority 2 while this workgroup loads, 0 in the butterflies and
+    // exchanges, 1 from the LOW FFT / store phase on: with three workgroups
+    // per CU in different phases, the loads and stores issue ahead of the
+    // co-resident workgroups' XOR networks.  One k = 512 square: RS 0.288 ->
+    // 0.276 ms; at 16 squares per launch (every slot busy) +3 %, so the engine
+    // sets job.prio for small batches only (profiles/r05/rs16_prio_ab.txt).
+    if (job.prio) __builtin_amdgcn_s_setprio(2);
     extern __shared__ u32x4 X[];
     const uint32_t tid = threadIdx.x;
     // Lane-derived values are recomputed from tid once per exchange call and
@@ -179,6 +186,7 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     bs16::phase_low_ifft<LOGK>(R, m, w);
 #endif
 
+    if (job.prio) __builtin_amdgcn_s_setprio(0);
     // ---- exchanges ------------------------------------------------------------
     // X12 / X21 (LOW <-> M1, within each wave): unit u of lane (b4, jl) <->
     // unit jl & 7 of lane (b4, (jl & 8) | u).  Slot ((chunk * NW + w) * 8 +
@@ -247,6 +255,7 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     bs16::phase_m1_fft<LOGK>(R, m, w);
     x12(true);
     lane_masks(m);
+    if (job.prio) __builtin_amdgcn_s_setprio(1);
     // ---- LOW FFT, planes -> bytes, store parity --------------------------------
     auto store = [&](auto uu) {
         constexpr int u = decltype(uu)::value;
