@@ -288,7 +288,8 @@ class Engine {
                     bool subtrees = false);
     int subtree_min_ = 8;   // CDA_SUBTREE: fused subtree levels of >= this many leaves (0 = off)
     uint64_t subtree_lanes_ = 0;   // CDA_SUBTREE_LANES: lanes a subtree launch must hold (0 = by tree size)
-    uint32_t rs16_prio_max_ = 4;   // CDA_RS16_PRIO_MAX: squares per launch up to which RsJob::prio is set
+    uint32_t rs16_prio_max_ = 4;   // CDA_RS16_PRIO_MAX: squares per launch up to which RsJob::prio is set (k >= 256)
+    bool rs8_prio_ = true;         // CDA_RS8_PRIO=0: no RsJob::prio for the GF(2^8) bitsliced encoder
     uint32_t top_fuse_nodes(uint32_t W, uint32_t n, bool* wide = nullptr) const;
     int top_fuse_ = -1;   // CDA_TOP_FUSE (tuning / A-B): -1 auto, 0 off, N = nodes per tree
     int top_wide_ = 2;    // CDA_TOP_WIDE: levels the tree top absorbs below the lane-pair level

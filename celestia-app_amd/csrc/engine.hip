@@ -227,6 +227,7 @@ int Engine::init() {
     if (const char* env = getenv("CDA_SUBTREE")) subtree_min_ = atoi(env);
     if (const char* env = getenv("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
     if (const char* env = getenv("CDA_RS16_PRIO_MAX")) rs16_prio_max_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = getenv("CDA_RS8_PRIO")) rs8_prio_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
     if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
     if (const char* env = getenv("CDA_FAULT")) fault_ = env;
@@ -379,7 +380,7 @@ int Engine::enqueue_extend(const uint8_t* d_ods, uint32_t k, uint32_t n, uint8_t
     RsJob q0 = d_ods ? square_job_q0(d_ods, d_eds, k) : square_job_q0_inplace(d_eds, k);
     RsJob q3 = square_job_q3(d_eds, k);
     q0.err_init = err_init;
-    q0.prio = q3.prio = n <= rs16_prio_max_ ? 1u : 0u;   // (read by the GF(2^16) bitsliced encoder only)
+    q0.prio = q3.prio = (k >= 256 ? n <= rs16_prio_max_ : rs8_prio_) ? 1u : 0u;
     if ((rc = check(launch_rs(q0, k, n, t, s), "rs Q0"))) return rc;
     mark_end(s);
     mark_begin(kStageRsQ3, s);

@@ -215,6 +215,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     const uint32_t d0 = g.dst_off + c * g.dst_cw + col + (16 * u + h) * g.dst_sh;
     uint32_t ud = threadIdx.x >> 6;   // divergent copy of u for the per-U chains (see rs8_bs_kernel)
     asm volatile("" : "+v"(ud));
+    // Wave priority 2 while loading, 0 in the passes, 1 from pass C (the
+    // stores) on, as in rs_gf16_bs.hip: the two co-resident workgroups' loads
+    // and stores issue ahead of the other's XOR networks.  Config 4's RS
+    // 8.73-8.78 -> 8.62-8.65 ms per 1 024 squares, 128 squares -3 %
+    // (profiles/r05/rs8_prio_ab.txt; CDA_RS8_PRIO=0 turns it off).
+    if (job.prio) __builtin_amdgcn_s_setprio(2);
 
     uint32_t R[64];
 #pragma unroll
@@ -240,6 +246,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     }
 #pragma unroll
     for (int j = 0; j < 8; j++) transpose8(R + 8 * j);
+    if (job.prio) __builtin_amdgcn_s_setprio(0);
     // ---- pass A: IFFT shard distance 1 (across the lane pair), then 2, 4, 8
     with_u_chain(ud, [&](auto U) {
         constexpr int UU = decltype(U)::value;
@@ -283,6 +290,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
             for (int pp = 0; pp < 4; pp++) R[8 * j + 4 * r + pp] = E[((j * 8 + u) * 4 + pp) * 64 + l];
     }
+    if (job.prio) __builtin_amdgcn_s_setprio(1);
     // ---- pass C: FFT shard distance 8, 4, 2, then 1 across the lane pair
     with_u_chain(ud, [&](auto U) {
         constexpr int UU = decltype(U)::value;
