@@ -218,8 +218,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     // Wave priority 2 while loading, 0 in the passes, 1 from pass C (the
     // stores) on, as in rs_gf16_bs.hip: the two co-resident workgroups' loads
     // and stores issue ahead of the other's XOR networks.  Config 4's RS
-    // 8.73-8.78 -> 8.62-8.65 ms per 1 024 squares, 128 squares -3 %
-    // (profiles/r05/rs8_prio_ab.txt; CDA_RS8_PRIO=0 turns it off).
+    // 8.73-8.78 -> 8.62-8.65 ms per 1 024 squares, 128 squares -3 % on one
+    // box (profiles/r05/rs8_prio_ab.txt), equal on another
+    // (final_vs_r05z_ab.txt); CDA_RS8_PRIO=0 turns it off.
     if (job.prio) __builtin_amdgcn_s_setprio(2);
 
     uint32_t R[64];
