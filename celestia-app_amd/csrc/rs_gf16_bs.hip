@@ -152,18 +152,6 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     // spills, but RS +6-8 % at batch 4; profiles/r05/leaf_overlap_lanemask_ab.txt.)
     uint32_t m[4];
     lane_masks(m);
-#if defined(CDA_BS16_SPLIT2)
-    // LOW IFFT layers 0 and 1 pair units within 0..3 and within 4..7: run them
-    // on units 0..3 while the loads of units 4..7 are still in flight (the
-    // wait for a unit's data sits before its planes transform).
-    bs16::sfor<0, 4, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
-    bs16::low_layer<LOGK, true, 0, 0, 4>(R, m, w);
-    bs16::low_layer<LOGK, true, 1, 0, 4>(R, m, w);
-    bs16::sfor<4, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
-    bs16::low_layer<LOGK, true, 0, 4, 8>(R, m, w);
-    bs16::low_layer<LOGK, true, 1, 4, 8>(R, m, w);
-    bs16::low_layer<LOGK, true, 2>(R, m, w);
-#elif !defined(CDA_BS16_NO_SPLIT)
     // LOW IFFT layer 0 pairs units (0,1), (2,3), ..., layer 1 pairs within
     // 0..3 and within 4..7: each pair / quad of units goes through the layers
     // it can as soon as its loads land (the wait for a unit's data sits
@@ -181,10 +169,6 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     planes2(std::integral_constant<int, 6>{});
     bs16::low_layer<LOGK, true, 1, 4, 8>(R, m, w);
     bs16::low_layer<LOGK, true, 2>(R, m, w);
-#else
-    bs16::sfor<0, 8, 1>([&](auto uu) { bs16::block_planes(R + 16 * decltype(uu)::value); });
-    bs16::phase_low_ifft<LOGK>(R, m, w);
-#endif
 
     if (job.prio) __builtin_amdgcn_s_setprio(0);
     // ---- exchanges ------------------------------------------------------------
@@ -268,16 +252,6 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
         for (int q = 0; q < 4; q++)
             p[q] = u32x4{R[16 * u + 4 * q], R[16 * u + 4 * q + 1], R[16 * u + 4 * q + 2], R[16 * u + 4 * q + 3]};
     };
-#if defined(CDA_BS16_SPLIT2)
-    // mirror of the entry: units 0..3 finish and store while 4..7 compute
-    bs16::low_layer<LOGK, false, 2>(R, m, w);
-    bs16::low_layer<LOGK, false, 1, 0, 4>(R, m, w);
-    bs16::low_layer<LOGK, false, 0, 0, 4>(R, m, w);
-    bs16::sfor<0, 4, 1>(store);
-    bs16::low_layer<LOGK, false, 1, 4, 8>(R, m, w);
-    bs16::low_layer<LOGK, false, 0, 4, 8>(R, m, w);
-    bs16::sfor<4, 8, 1>(store);
-#elif !defined(CDA_BS16_NO_SPLIT)
     // mirror of the entry: each pair of units stores as soon as it is done
     auto store2 = [&](auto uu) {
         constexpr int u = decltype(uu)::value;
@@ -292,10 +266,6 @@ __global__ __launch_bounds__(64 << (LOGK - 7)) __attribute__((amdgpu_waves_per_e
     bs16::low_layer<LOGK, false, 1, 4, 8>(R, m, w);
     store2(std::integral_constant<int, 4>{});
     store2(std::integral_constant<int, 6>{});
-#else
-    bs16::phase_low_fft<LOGK>(R, m, w);
-    bs16::sfor<0, 8, 1>(store);
-#endif
 }
 
 template <int LOGK>

@@ -4,7 +4,9 @@
 # as soon as their loads land, and stores each pair of units as soon as LOW
 # FFT is done with it; build_var/split2/libcda.so (-DCDA_BS16_SPLIT2) splits
 # only into halves, build_var/nosplit/libcda.so (-DCDA_BS16_NO_SPLIT) not at
-# all.  Then a kernel trace of the timed region of each (TRACE=1).  Parity of the product build first
+# all.  Then a kernel trace of the timed region of each (TRACE=1).  The two
+# variants left the product source in round 5: apply
+# tools/probes/rs16_split_variants.patch before building them.  Parity of the product build first
 # (every k = 512 / GF(2^16) GPU test), then interleaved bench runs at batch
 # 1 / 4 / 16.  Output: gpurun_out/<tag>/.
 set -o pipefail
