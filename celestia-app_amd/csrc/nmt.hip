@@ -530,7 +530,11 @@ __device__ __forceinline__ void data_root_level(const uint32_t* __restrict__ in,
     }
 }
 
-constexpr uint32_t kPairMaxParents = 128;   // 256 lanes: one wave per SIMD of the CU
+// 512 lanes: two waves per SIMD of the CU.  (128 until round 5: a k = 512
+// square's 256-parent first data-root level then ran a thread per parent;
+// on lane pairs in a 512-thread launch the data root 0.055 -> 0.049 ms,
+// profiles/r05/data_root_pairs_ab.txt.)
+constexpr uint32_t kPairMaxParents = 256;
 
 // 16 rounds [R0, R0 + 16) of a lane-pair compression over precomputed
 // K + W words (v: the pair's 4 state words, as in sha_pair_compress).
