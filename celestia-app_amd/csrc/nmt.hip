@@ -530,11 +530,14 @@ __device__ __forceinline__ void data_root_level(const uint32_t* __restrict__ in,
     }
 }
 
-// 512 lanes: two waves per SIMD of the CU.  (128 until round 5: a k = 512
-// square's 256-parent first data-root level then ran a thread per parent;
-// on lane pairs in a 512-thread launch the data root 0.055 -> 0.049 ms,
-// profiles/r05/data_root_pairs_ab.txt.)
-constexpr uint32_t kPairMaxParents = 256;
+// Largest data-root level run on lane pairs: 128 parents (256 lanes, a wave
+// per SIMD), or 256 in launches of few squares (kPairMaxParentsSmall, 512
+// lanes: a k = 512 square's first level; data root 0.055 -> 0.049 ms,
+// profiles/r05/data_root_pairs_ab.txt -- at config 4's 1 024 squares the
+// 512-thread launch made the stage 0.143 -> 0.209 ms, so not there).
+constexpr uint32_t kPairMaxParents = 128;
+constexpr uint32_t kPairMaxParentsSmall = 256;
+constexpr uint32_t kPairSmallSquares = 8;   // launches of <= this many squares
 
 // 16 rounds [R0, R0 + 16) of a lane-pair compression over precomputed
 // K + W words (v: the pair's 4 state words, as in sha_pair_compress).
@@ -685,9 +688,9 @@ __device__ __forceinline__ void data_root_levels(const uint32_t* D, uint32_t n, 
     for (uint32_t m = n / 2; m >= 1; m >>= 1) {
         const uint32_t* in = m == n / 2 ? D : src;
         uint32_t* out = m == n / 2 ? src : dst;
-        if (pair_ok == 2 && m <= 32 && blockDim.x >= 128)
+        if ((pair_ok & 0xFF) == 2 && m <= 32 && blockDim.x >= 128)
             data_root_level_helped(in, out, m, kwb);
-        else if (pair_ok && m <= kPairMaxParents && 2 * m <= blockDim.x)
+        else if ((pair_ok & 0xFF) && m <= (pair_ok >> 8 ? pair_ok >> 8 : kPairMaxParents) && 2 * m <= blockDim.x)
             data_root_level<true>(in, out, m);
         else
             data_root_level<false>(in, out, m);
@@ -1232,10 +1235,12 @@ hipError_t launch_data_root_digests(const uint32_t* dig, uint32_t n_items, uint3
     }
     // a thread per first-level parent (<= 512: more would cap the kernel at
     // 128 VGPRs and spill the helpers' registers), and room for the lane pairs
+    const uint32_t pmax = n <= kPairSmallSquares ? kPairMaxParentsSmall : kPairMaxParents;
     uint32_t threads = std::min<uint32_t>(n_items / 2, 512);
-    threads = std::max<uint32_t>(threads, std::min<uint32_t>(n_items, 2 * kPairMaxParents));
+    threads = std::max<uint32_t>(threads, std::min<uint32_t>(n_items, 2 * pmax));
     threads = std::max<uint32_t>((threads + 63) / 64 * 64, 64);
-    const uint32_t mode = data_root_mode();
+    // mode in the low byte, the largest pair level above it
+    const uint32_t mode = data_root_mode() | pmax << 8;
     hipLaunchKernelGGL(data_root_digest_kernel, dim3(n), dim3(threads), lds, s, dig, n_items, data_roots,
                        status ? err : nullptr, status, mode);
     return hipGetLastError();
