@@ -565,9 +565,11 @@ def config5(ctx, dev, rank: int, world: int, k: int, iters: int = 5, emit=None) 
         dist.broadcast(uid, src=0)
         c = _lib.Context(dev.index)
         c.comm_init(rank, world, bytes(uid.cpu().numpy()))
+        comm_rank, comm_world = c.comm_size()
         el, res = timed(lambda: cdist.extend_dah_split_rccl(c, mine, k, rank, world))
         el, bad = max_over_ranks(el, 0)
-        out["library_rccl"] = {"ms_per_square": 1e3 * el / iters, "squares_per_s": iters / el}
+        out["library_rccl"] = {"ms_per_square": 1e3 * el / iters, "squares_per_s": iters / el,
+                               "communicator_ranks": comm_world}
         if rank == 0:
             out["library_rccl"]["matches_single_gpu"] = matches(res[1])
         c.comm_destroy()
@@ -842,6 +844,84 @@ def blob_commitments(ctx, dev, stream, n_blocks: int = 64, reps: int = 10) -> di
             "workload": f"all blobs of {n_blocks} full k=128 blocks (CheckTx/ProcessProposal ValidateBlobTx)"}
 
 
+def launch_mode(gpus: int, env) -> str:
+    """How `bench.py --gpus N` runs:
+    - WORLD_SIZE set (torch.distributed.run or our own spawn): this process is
+      one rank; WORLD_SIZE must equal --gpus, else the run is refused
+      ("mismatch") instead of silently measuring another world size;
+    - WORLD_SIZE unset and N == 1: one rank in this process ("inprocess");
+    - WORLD_SIZE unset and N > 1: this process stays GPU-free and starts N
+      rank processes itself ("spawn")."""
+    if gpus < 1:
+        return "mismatch"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and ws != "":
+        return "rank" if int(ws) == gpus else "mismatch"
+    return "inprocess" if gpus == 1 else "spawn"
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_commands(argv: list, gpus: int, port: int, env) -> list:
+    """(argv, env) of each rank process of a self-spawned N-rank run: the same
+    script and arguments, with the env:// rendezvous variables
+    torch.distributed.run would set (RANK = LOCAL_RANK = g, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1, a free MASTER_PORT)."""
+    out = []
+    for g in range(gpus):
+        e = dict(env)
+        e.update({"RANK": str(g), "LOCAL_RANK": str(g), "WORLD_SIZE": str(gpus), "LOCAL_WORLD_SIZE": str(gpus),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                  "CDA_BENCH_LAUNCHER": "bench.py"})
+        out.append(([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), e))
+    return out
+
+
+def _exit_status(rc: int) -> int:
+    return rc if rc > 0 else 128 - rc    # -N (killed by signal N) -> 128 + N, as a shell reports it
+
+
+def spawn_ranks(argv: list, gpus: int, grace_s: float = 60.0) -> int:
+    """Run N rank processes (children, never an exec: this parent has not
+    touched the GPU and does not import torch).  Rank 0 prints the JSON line
+    on the inherited stdout.  When a rank fails, the others get `grace_s` to
+    finish (they may be blocked in a collective with it), then their process
+    groups are killed.  Returns the first non-zero exit status, else 0."""
+    import signal
+    import subprocess
+    procs = []
+    for cmd, env in rank_commands(argv, gpus, free_port(), os.environ):
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    rc, failed_at = 0, None
+    try:
+        while any(p.poll() is None for p in procs):
+            for g, p in enumerate(procs):
+                if p.returncode not in (None, 0) and rc == 0:
+                    rc, failed_at = _exit_status(p.returncode), time.monotonic()
+                    print(f"bench.py: rank {g} exited with {p.returncode}", file=sys.stderr, flush=True)
+            if failed_at is not None and time.monotonic() - failed_at > grace_s:
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    for g, p in enumerate(procs):
+        if rc == 0 and p.returncode != 0:
+            rc = _exit_status(p.returncode)
+            print(f"bench.py: rank {g} exited with {p.returncode}", file=sys.stderr, flush=True)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -865,6 +945,14 @@ def main():
                          "rsmt2d's EDS has; no Q0 copy); packed: ODS in its own k*k buffer "
                          "(cda_extend_dah_device, Q0 copied into the EDS)")
     args = ap.parse_args()
+
+    mode = launch_mode(args.gpus, os.environ) if not args.config5_child else "rank"
+    if mode == "mismatch":
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}: refusing to measure a "
+              f"different world size than asked", file=sys.stderr)
+        sys.exit(2)
+    if mode == "spawn":   # before torch is imported: the parent never touches the GPU
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
 
     import numpy as np
     import torch
@@ -890,6 +978,11 @@ def main():
             os.environ.setdefault("WORLD_SIZE", "1")
         backend = os.environ.get("CDA_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+    launch = {"mode": {"rank": "external launcher" if not os.environ.get("CDA_BENCH_LAUNCHER")
+                       else "spawned by bench.py --gpus", "inprocess": "single process"}[mode],
+              "group_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+              "backend": dist.get_backend() if dist.is_initialized() else None}
 
     if args.config5_child:   # config5_isolated's child: one rank of config 5, JSON on stdout (rank 0)
         def emit(part):
@@ -963,6 +1056,14 @@ def main():
         t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    if world > 1:   # every rank's shard is checked against the fixture; the line reports all of them
+        pt = torch.tensor([parity["checked"], parity["matched"]], dtype=torch.int64,
+                          device=dev if dist.get_backend() == "nccl" else "cpu")
+        allp = [torch.zeros_like(pt) for _ in range(world)]
+        dist.all_gather(allp, pt)
+        per = [[int(x[0]), int(x[1])] for x in allp]
+        parity = {"checked": sum(c for c, _ in per), "matched": sum(m for _, m in per), "per_rank": per}
 
     # the timed region runs the product path exactly as a caller would (no
     # stage events); the per-stage HIP-event breakdown comes from a separate
@@ -1195,6 +1296,7 @@ def main():
             "value": value,
             "unit": "squares/s",
             "n_gpus": world,
+            "launch": launch,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * el / args.steps,
@@ -1218,9 +1320,11 @@ def main():
             "ods_gb_per_s": value * k * k * SHARE / 1e9,
             "stage_pass": {"steps": n_prof, "ms_per_step": 1e3 * el_prof / n_prof,
                            "note": "stages and rooflines come from this separate pass with HIP events at every "
-                                   "stage border, on the one-stream schedule (with profiling on the library "
-                                   "does not split the hash stages over two streams); value / ms_per_step come "
-                                   "from the event-free timed region with the default two-stream hash split"},
+                                   "stage border, on the one-stream schedule; value / ms_per_step come from the "
+                                   "event-free timed region, whose hash stages run on " +
+                                   ("two streams (enqueue_dah splits batches of < 64 squares at k <= 128)"
+                                    if B < 64 and k <= 128 else
+                                    "one stream (enqueue_dah splits only batches of < 64 squares at k <= 128)")},
             "roofline": roofline,
             "rs_roofline": rs_roof,
             "traffic": traffic,

@@ -15,6 +15,10 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("CDA_LIB", os.path.join(PKG_ROOT, "libcda.so"))
+# The test build (make -C celestia-app_amd test-lib; -DCDA_TESTING): the same
+# kernels, plus the test knobs -- fault injection and A/B schedule switches --
+# that libcda.so never reads (csrc/knobs.h).  Only tests load it.
+TEST_LIB_PATH = os.path.join(PKG_ROOT, "libcda_test.so")
 
 SHARE_SIZE = 512
 NAMESPACE_SIZE = 29
@@ -55,14 +59,14 @@ EXPORTED = (
     "cda_ctx_create", "cda_ctx_destroy", "cda_last_error", "cda_version", "cda_extend_shares",
     "cda_dah_from_eds", "cda_extend_dah", "cda_extend_dah_batch", "cda_extend_dah_device",
     "cda_extend_dah_inplace_device", "cda_reserve",
-    "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_set_profiling", "cda_stage_times",
+    "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_push_order_detail_at", "cda_set_profiling", "cda_stage_times",
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
     "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
     "cda_blob_commitments", "cda_blob_commitments_device",
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
     "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
-    "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_comm_abort", "cda_extend_dah_split", "cda_split_rows_send",
+    "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_comm_size", "cda_comm_abort", "cda_extend_dah_split", "cda_split_rows_send",
     "cda_extend_dah_multi", "cda_split_layout", "cda_split_offsets", "cda_extend_dah_batch_ex",
 )
 STAGES = ("rs_q0", "rs_q3", "order_check", "nmt_leaves", "nmt_levels", "data_root")
@@ -104,25 +108,28 @@ class SplitLayoutT(C.Structure):
 
 
 _lib = None
+_libs = {}
 _lock = threading.RLock()   # re-entrant: default_context() creates a Context (load()) under it
 
 
-def load():
-    """Load libcda.so and declare prototypes. Raises OSError if absent."""
+def load(path: str | None = None):
+    """Load libcda.so (or the library at `path`, e.g. TEST_LIB_PATH) and
+    declare prototypes. Raises OSError if absent."""
     global _lib
+    path = path or LIB_PATH
     with _lock:
-        if _lib is not None:
-            return _lib
+        if path in _libs:
+            return _libs[path]
         # One HIP runtime per process: PyTorch-ROCm bundles its own
         # libamdhip64 (same soname).  If libcda.so were loaded first, a later
         # `import torch` would map a second runtime and see no GPU; importing
         # torch first makes libcda bind to torch's copy.
         if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
             import torch  # noqa: F401
-        if not os.path.exists(LIB_PATH):
-            raise OSError(f"libcda.so not built at {LIB_PATH}; run __graft_entry__.build() "
+        if not os.path.exists(path):
+            raise OSError(f"{os.path.basename(path)} not built at {path}; run __graft_entry__.build() "
                           "(no CPU fallback exists)")
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
         u8p = C.POINTER(C.c_uint8)
         vp = C.c_void_p
         ctxp = C.c_void_p
@@ -145,6 +152,8 @@ def load():
         L.cda_data_root.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p]
         L.cda_push_order_detail.argtypes = [ctxp, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
                                             C.POINTER(C.c_uint32)]
+        L.cda_push_order_detail_at.argtypes = [ctxp, C.c_uint32, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                               C.POINTER(C.c_uint32)]
         L.cda_split_rows.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.cda_split_cols.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
         L.cda_split_combine.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
@@ -179,6 +188,7 @@ def load():
         L.cda_comm_init.argtypes = [ctxp, C.c_int, C.c_int, u8p]
         L.cda_comm_destroy.argtypes = [ctxp]
         L.cda_comm_abort.argtypes = [ctxp]
+        L.cda_comm_size.argtypes = [ctxp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.cda_extend_dah_split.argtypes = [ctxp, vp, C.c_uint32, vp, vp, vp, vp, vp, vp]
         L.cda_split_rows_send.argtypes = [ctxp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.cda_extend_dah_multi.argtypes = [C.POINTER(ctxp), C.c_uint32, u8p, C.c_uint32, C.c_uint32, u8p, u8p, u8p,
@@ -187,7 +197,9 @@ def load():
         L.cda_split_offsets.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, u32p, u32p, u64p]
         L.cda_set_profiling.argtypes = [ctxp, C.c_int]
         L.cda_stage_times.argtypes = [ctxp, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int]
-        _lib = L
+        _libs[path] = L
+        if path == LIB_PATH:
+            _lib = L
         return L
 
 
@@ -225,8 +237,8 @@ def ptr(a: np.ndarray | None):
 class Context:
     """One libcda context (HIP device + stream)."""
 
-    def __init__(self, device: int = -1):
-        self.lib = load()
+    def __init__(self, device: int = -1, lib_path: str | None = None):
+        self.lib = load(lib_path)
         h = C.c_void_p()
         rc = self.lib.cda_ctx_create(device, C.byref(h))
         if rc != CDA_OK:
@@ -308,6 +320,12 @@ class Context:
     def comm_destroy(self):
         self.check(self.lib.cda_comm_destroy(self.h))
 
+    def comm_size(self) -> tuple:
+        """(rank, world) as the library's RCCL communicator formed them."""
+        r, w = C.c_int(), C.c_int()
+        self.check(self.lib.cda_comm_size(self.h, C.byref(r), C.byref(w)))
+        return r.value, w.value
+
     def comm_abort(self):
         """ncclCommAbort (safe from a watchdog thread while a call waits)."""
         self.check(self.lib.cda_comm_abort(self.h))
@@ -320,6 +338,13 @@ class Context:
     def push_order_detail(self):
         a, i, p = C.c_int32(), C.c_uint32(), C.c_uint32()
         self.lib.cda_push_order_detail(self.h, C.byref(a), C.byref(i), C.byref(p))
+        return a.value, i.value, p.value
+
+    def push_order_detail_at(self, square: int):
+        """(axis, index, position) of square `square` of the last device
+        batch (axis -1: ordered); waits for that batch's GPU work."""
+        a, i, p = C.c_int32(), C.c_uint32(), C.c_uint32()
+        self.check(self.lib.cda_push_order_detail_at(self.h, square, C.byref(a), C.byref(i), C.byref(p)))
         return a.value, i.value, p.value
 
 

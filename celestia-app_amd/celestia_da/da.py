@@ -222,6 +222,19 @@ def min_data_availability_header() -> DataAvailabilityHeader:
     return new_data_availability_header(extend_shares(min_shares()))
 
 
+def _batch_shape(ods: np.ndarray) -> tuple:
+    """(n, k) of a batch shaped (n, k*k, 512) or (n, k, k, 512); k from the
+    shape, never rounded.  n may be 0 (an empty batch: the C API
+    returns CDA_OK and the outputs are empty)."""
+    if ods.ndim == 4 and ods.shape[1] == ods.shape[2] and ods.shape[3] == SHARE_SIZE:
+        return ods.shape[0], ods.shape[1]
+    if ods.ndim == 3 and ods.shape[2] == SHARE_SIZE:
+        k = int(round(ods.shape[1] ** 0.5))
+        if k * k == ods.shape[1]:
+            return ods.shape[0], k
+    raise ValueError(f"batch must be shaped (n, k*k, {SHARE_SIZE}) or (n, k, k, {SHARE_SIZE}), got {ods.shape}")
+
+
 def extend_dah_batch_parity(ods: np.ndarray, ctx=None, skip_q0: bool = False):
     """cda_extend_dah_batch_ex: the batch's roots and its parity only.
 
@@ -231,8 +244,7 @@ def extend_dah_batch_parity(ods: np.ndarray, ctx=None, skip_q0: bool = False):
     (parity, rows, cols, data_roots, status)."""
     ctx = ctx or default_context()
     ods = np.ascontiguousarray(ods, dtype=np.uint8)
-    n = ods.shape[0]
-    k = int(round((ods.size // (n * SHARE_SIZE)) ** 0.5))
+    n, k = _batch_shape(ods)
     W = 2 * k
     if skip_q0:
         out = np.zeros((n, W, W, SHARE_SIZE), dtype=np.uint8)
@@ -268,8 +280,7 @@ def extend_dah_batch(ods: np.ndarray, want_eds: bool = True, ctx=None):
     """Batch of n squares (n, k*k, 512) -> (eds|None, rows, cols, data_roots, status)."""
     ctx = ctx or default_context()
     ods = np.ascontiguousarray(ods, dtype=np.uint8)
-    n = ods.shape[0]
-    k = int(round((ods.size // (n * SHARE_SIZE)) ** 0.5))
+    n, k = _batch_shape(ods)
     W = 2 * k
     eds = np.empty((n, W, W, SHARE_SIZE), dtype=np.uint8) if want_eds else None
     rows = np.empty((n, W, NMT_ROOT_SIZE), dtype=np.uint8)

@@ -139,7 +139,7 @@ int plan_square(const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs, uint
 
 extern "C" {
 
-const char* cda_version(void) { return "cda 0.1.0 gfx950"; }
+const char* cda_version(void) { return cda::kTestBuild ? "cda 0.1.0 gfx950 test-build" : "cda 0.1.0 gfx950"; }
 
 int cda_ctx_create(int device, cda_ctx** out) {
     if (!out) return CDA_ERR_INVALID;
@@ -224,6 +224,7 @@ int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t 
             return e.fail(CDA_ERR_INVALID, "null buffer");
         uint32_t* err = e.err_words(n);
         if (!err) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
+        e.set_device_batch(n);
         return e.enqueue_extend_dah(static_cast<const uint8_t*>(d_ods), k, n, static_cast<uint8_t*>(d_eds),
                                     static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
                                     static_cast<uint8_t*>(d_data_roots), err, d_status, s);
@@ -245,6 +246,7 @@ int cda_extend_dah_inplace_device(cda_ctx* ctx, uint32_t k, uint32_t n, void* d_
         if (!d_eds || !d_row_roots || !d_col_roots || !d_data_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
         uint32_t* err = e.err_words(n);
         if (!err) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
+        e.set_device_batch(n);
         return e.enqueue_extend_dah(nullptr, k, n, static_cast<uint8_t*>(d_eds), static_cast<uint8_t*>(d_row_roots),
                                     static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_data_roots), err,
                                     d_status, s);
@@ -282,6 +284,13 @@ int cda_push_order_detail(cda_ctx* ctx, int32_t* axis, uint32_t* index, uint32_t
     if (index) *index = tl_err.index;
     if (position) *position = tl_err.pos;
     return CDA_OK;
+}
+
+int cda_push_order_detail_at(cda_ctx* ctx, uint32_t square, int32_t* axis, uint32_t* index, uint32_t* position) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!axis || !index || !position) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.device_push_order_detail(square, axis, index, position);
+    });
 }
 
 int cda_split_rows(cda_ctx* ctx, const void* d_ods_rows, uint32_t k, uint32_t n_rows, uint32_t row0,
@@ -476,7 +485,10 @@ int cda_square_destroy(cda_square* sq) {
     if (!sq) return CDA_OK;
     std::lock_guard<std::mutex> g(sq->ctx->eng.mutex());
     DeviceScope dev(sq->ctx->eng.device());
-    (void)sq->ctx->eng.drain();   // no queued work of the context reads the square any more
+    // no queued work of the context reads the square any more: the square's
+    // calls end with the context's end event, and waiting for that (not every
+    // context stream) leaves unrelated in-flight batch work alone
+    (void)sq->ctx->eng.wait_last_call();
     delete sq;
     return CDA_OK;
 }
@@ -621,6 +633,13 @@ int cda_comm_destroy(cda_ctx* ctx) {
     return guarded(ctx, [&](cda::Engine& e) -> int {
         e.comm_destroy();
         return CDA_OK;
+    });
+}
+
+int cda_comm_size(cda_ctx* ctx, int* rank, int* world) {
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        if (!rank || !world) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.comm_size(rank, world);
     });
 }
 

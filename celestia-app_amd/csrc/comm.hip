@@ -13,6 +13,7 @@
 //     no collective at all.
 // Reference call sites: app/process_proposal.go:138-152 (block replay),
 // pkg/da/data_availability_header.go:44-75.
+#include "knobs.h"
 #include <rccl/rccl.h>
 
 #include <chrono>
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void group_rows_kernel(const uint4* __restrict
 // (this rank's scratch allocation in the agreement round).  Lets the GPU
 // tests drive every error path at world size 1.
 bool comm_fault(const char* where) {
-    const char* e = getenv("CDA_COMM_FAULT");
+    const char* e = test_knob("CDA_COMM_FAULT");
     return e && strcmp(e, where) == 0;
 }
 
@@ -146,6 +147,18 @@ int Engine::comm_fail(const char* what, int result) {
     world_ = 0;
     comm_k_ = 0;
     return fail(CDA_ERR_COMM, msg);
+}
+
+// The communicator's own view (ncclCommUserRank / ncclCommCount), so a host
+// can report the world size RCCL actually formed.
+int Engine::comm_size(int* rank, int* world) {
+    std::lock_guard<std::mutex> g(comm_mu_);
+    if (!comm_) return fail(CDA_ERR_INVALID, "no communicator: call cda_comm_init first");
+    ncclComm_t c = static_cast<ncclComm_t>(comm_);
+    ncclResult_t r = ncclCommCount(c, world);
+    if (r == ncclSuccess) r = ncclCommUserRank(c, rank);
+    if (r != ncclSuccess) return fail(CDA_ERR_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+    return CDA_OK;
 }
 
 int Engine::comm_abort() {

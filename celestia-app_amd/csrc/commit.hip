@@ -31,6 +31,7 @@
 //      equal to the RFC split rule).
 // VALU-bound like the EDS hashing: 9 compressions per share + 3 per inner node
 // + 2 per subtree root and RFC node.
+#include "knobs.h"
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -623,7 +624,7 @@ hipError_t launch_slot_merkle_roots(const uint8_t* slots, const uint32_t* bt, ui
 // groups (A/B knob, read once).
 static bool group_commitments() {
     static const bool on = [] {
-        const char* e = std::getenv("CDA_COMMIT_GROUP");
+        const char* e = test_knob("CDA_COMMIT_GROUP");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -631,7 +632,7 @@ static bool group_commitments() {
 // CDA_COMMIT_FUSED=0: small-blob batches also take the level launches and
 // commitment_group_kernel instead of commitment_fused_kernel (read per call).
 static bool fuse_commitments() {
-    const char* e = std::getenv("CDA_COMMIT_FUSED");
+    const char* e = test_knob("CDA_COMMIT_FUSED");
     return !(e && e[0] == '0');
 }
 
@@ -702,7 +703,7 @@ int Engine::enqueue_commitments(const square::CommitPlan& p, uint32_t n_blobs, c
         for (uint32_t b = 0; b < n_blobs; b++) units += (bt[b + 1] - bt[b]) / 2;
         // CDA_COMMIT_UCAP (read per call; tests): a larger minimum, to drive
         // the lane-per-unit passes with small batches
-        const char* ue = std::getenv("CDA_COMMIT_UCAP");
+        const char* ue = test_knob("CDA_COMMIT_UCAP");
         const uint64_t umin = ue ? std::max(1L, std::atol(ue)) : 32;
         const uint32_t ucap = (uint32_t)std::max<uint64_t>(umin, (units + 1023) / 1024);
         const uint32_t tcap = std::max(p.max_trees, 512u);

@@ -2,6 +2,7 @@
 // HIP stream, the GF(2^16) tables and grow-only scratch buffers, and the
 // enqueue logic of the whole ODS -> EDS -> roots -> data-root pipeline.
 #pragma once
+#include "knobs.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -142,19 +143,28 @@ class Engine {
     // drain_streams + the last call's end on the caller's stream (order_ev_):
     // nothing of the context runs any more (destructors, resident squares).
     int drain();
-    // Tests only (CDA_FAULT, read at init): an injected error at a named point
+    // The last call's end on the caller's stream only (order_ev_): every call
+    // joins its side streams on success and a failed call drained them
+    // (capi.hip guarded), so this covers all GPU work any call queued.
+    int wait_last_call();
+    // Test build only (CDA_FAULT, read at init by libcda_test.so; knobs.h): an injected error at a named point
     // after GPU work was enqueued -- "dah_part" (enqueue_dah's side part, after
     // its leaves and levels), "pipe_chunk" (host_pipeline, after chunk 1's
     // compute), "extend_chunk" (the RS pipeline, after chunk 0's RS).  Fires
     // once per context, so the follow-up calls of a test run clean.
     bool fault_at(const char* where) {
-        if (fault_.empty() || fault_ != where) return false;
+        if (!kTestBuild || fault_.empty() || fault_ != where) return false;
         fault_.clear();
         return true;
     }
     // n push-order error words of a device entry point (context scratch), or
     // NULL when the allocation fails.
     uint32_t* err_words(uint32_t n) { return dev_err_.ensure((size_t)n * 4) == hipSuccess ? dev_err_.as<uint32_t>() : nullptr; }
+    // The push-order words belong to the last device batch of n squares
+    // (cda_extend_dah_device / _inplace_device): device_push_order_detail
+    // reads square sq's word after that batch's work completed.
+    void set_device_batch(uint32_t n) { dev_err_n_ = n; }
+    int device_push_order_detail(uint32_t sq, int32_t* axis, uint32_t* index, uint32_t* pos);
 
     // Enqueue the full path for n squares of width k (device pointers).
     // d_err: n u32 words (min-encoded push-order violation, ~0 = ordered);
@@ -189,6 +199,7 @@ class Engine {
                                 uint8_t* d_send, uint32_t* d_err, hipStream_t s);
     int comm_init(int rank, int world, const uint8_t* id);
     void comm_destroy();
+    int comm_size(int* rank, int* world);   // ncclCommUserRank / ncclCommCount of the live communicator
     int comm_abort();   // ncclCommAbort (e.g. from a host watchdog after a peer failed)
     int comm_rank() const { return rank_; }
     int split_extend_dah(const uint8_t* d_rows, uint32_t k, uint8_t* d_col_block, uint8_t* d_row_roots,
@@ -266,6 +277,7 @@ class Engine {
     void set_profiling(bool on) { profiling_ = on; }
     int collect_stage_times(double* ms, uint32_t* counts, int n);
 
+    uint32_t dev_err_n_ = 0;   // squares of the last device batch (their push-order words in dev_err_)
     int32_t po_axis = -1;
     uint32_t po_index = 0, po_pos = 0;
 

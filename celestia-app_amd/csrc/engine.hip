@@ -7,6 +7,7 @@
 //      with the Q0 namespace push-order check       (nmt Push, ErrInvalidPushOrder)
 //   4. log2(W) NMT levels over all 2W trees         (NmtHasher.HashNode)
 //   5. RFC-6962 data root                           (DataAvailabilityHeader.Hash)
+#include "knobs.h"
 #include "engine.h"
 
 #include <algorithm>
@@ -102,7 +103,7 @@ Engine::~Engine() {
                       &cm_leaf_, &cm_lvl_, &cm_roots_, &cm_out_, &gf8_log_, &gf8_exp_, &gf8_skew_, &rp_cw_,
                       &rp_err_, &rp_present_, &rp_parity_, &rp_buf_, &rp_flags_, &tr_cells_, &tr_levels_,
                       &tr_axis_, &tr_roots_, &rs_pad_, &split_blk_, &split_send_, &split_col_, &split_slots_,
-                      &comm_flag_})
+                      &comm_flag_, &h_par_})
         b->release();
     if (sq_event_) (void)hipEventSynchronize(sq_event_), (void)hipEventDestroy(sq_event_);
     if (sq_stage_) (void)hipHostFree(sq_stage_);
@@ -210,27 +211,27 @@ int Engine::init() {
             if ((rc = check(hipEventCreateWithFlags(&e[i], hipEventDisableTiming), "hipEventCreate"))) return rc;
     // CDA_RS_PRIORITY (tuning): priority of the pipeline's RS stream (HIP: a
     // lower value is a higher priority).
-    if (const char* env = getenv("CDA_RS_PRIORITY")) {
+    if (const char* env = test_knob("CDA_RS_PRIORITY")) {
         if ((rc = check(hipStreamCreateWithPriority(&aux_stream_, hipStreamNonBlocking, atoi(env)), "hipStreamCreate")))
             return rc;
     } else if ((rc = check(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking), "hipStreamCreate"))) {
         return rc;
     }
-    if (const char* env = getenv("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
-    if (const char* env = getenv("CDA_HASH_SPLIT")) hash_split_ = atoi(env);
-    if (const char* env = getenv("CDA_HOST_CHUNK")) host_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
-    if (const char* env = getenv("CDA_HOST_PIPE_CHUNK")) host_pipe_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
-    if (const char* env = getenv("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
-    if (const char* env = getenv("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
-    if (const char* env = getenv("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
-    if (const char* env = getenv("CDA_TOP_WIDE")) top_wide_ = atoi(env);
-    if (const char* env = getenv("CDA_SUBTREE")) subtree_min_ = atoi(env);
-    if (const char* env = getenv("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
-    if (const char* env = getenv("CDA_RS16_PRIO_MAX")) rs16_prio_max_ = (uint32_t)strtoul(env, nullptr, 10);
-    if (const char* env = getenv("CDA_RS8_PRIO")) rs8_prio_ = atoi(env) != 0;
-    if (const char* env = getenv("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
-    if (const char* env = getenv("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
-    if (const char* env = getenv("CDA_FAULT")) fault_ = env;
+    if (const char* env = deploy_knob("CDA_PIPELINE_CHUNK")) pipeline_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = test_knob("CDA_HASH_SPLIT")) hash_split_ = atoi(env);
+    if (const char* env = test_knob("CDA_HOST_CHUNK")) host_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = deploy_knob("CDA_HOST_PIPE_CHUNK")) host_pipe_chunk_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = test_knob("CDA_HOST_FULL_D2H")) host_full_d2h_ = atoi(env) != 0;
+    if (const char* env = deploy_knob("CDA_HOST_REGISTER")) host_register_ = atoi(env) != 0;
+    if (const char* env = test_knob("CDA_TOP_FUSE")) top_fuse_ = atoi(env);
+    if (const char* env = test_knob("CDA_TOP_WIDE")) top_wide_ = atoi(env);
+    if (const char* env = test_knob("CDA_SUBTREE")) subtree_min_ = atoi(env);
+    if (const char* env = test_knob("CDA_SUBTREE_LANES")) subtree_lanes_ = strtoull(env, nullptr, 10);
+    if (const char* env = test_knob("CDA_RS16_PRIO_MAX")) rs16_prio_max_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = test_knob("CDA_RS8_PRIO")) rs8_prio_ = atoi(env) != 0;
+    if (const char* env = test_knob("CDA_RS_CUS")) rs_cus_ = (uint32_t)strtoul(env, nullptr, 10);
+    if (const char* env = deploy_knob("CDA_SYNC_CHECK")) sync_check_ = atoi(env) != 0;
+    if (const char* env = test_knob("CDA_FAULT")) fault_ = env;
     // GF(2^16) tables (leopard.go initLUTs / initFFT), built on the host once.
     auto F = std::make_unique<LeoField<16>>();
     leo_build<16>(*F, 0x1002D, kCantor16);
@@ -311,13 +312,15 @@ int Engine::drain_streams() {
     return first;
 }
 
+int Engine::wait_last_call() {
+    if (order_used_ && order_ev_) return check(hipEventSynchronize(order_ev_), "hipEventSynchronize (last call)");
+    return CDA_OK;
+}
+
 int Engine::drain() {
     int rc = drain_streams();
-    if (order_used_ && order_ev_) {
-        const hipError_t e = hipEventSynchronize(order_ev_);
-        if (e != hipSuccess && rc == CDA_OK) rc = check(e, "hipEventSynchronize (drain)");
-    }
-    return rc;
+    const int w = wait_last_call();
+    return rc != CDA_OK ? rc : w;
 }
 
 void Engine::order_end(hipStream_t s) {
@@ -807,7 +810,7 @@ int Engine::make_cu_streams() {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_) != hipSuccess || ncu <= 0 ||
         rs_cus_ >= (uint32_t)ncu)
-        return fail(CDA_ERR_INVALID, "CDA_RS_CUS must be below the device's CU count");
+        return fail(CDA_ERR_INVALID, "the RS CU partition must be below the device's CU count");
     std::vector<uint32_t> rs((ncu + 31) / 32, 0u), hs((ncu + 31) / 32, 0u);
     for (uint32_t j = 0; j < rs_cus_; j++) {
         const uint32_t b = (33u * j) % (uint32_t)ncu;
@@ -927,6 +930,29 @@ int Engine::enqueue_rs(const uint8_t* d_data, uint8_t* d_parity, uint32_t k, uin
     return check(launch_rs16_flat(gf16(k), d_data, d_parity, k, len, n, s), "rs16 flat");
 }
 
+// cda_push_order_detail_at: the decoded push-order word of square sq of the
+// last device batch, once that batch's GPU work (the call's end event) is done.
+int Engine::device_push_order_detail(uint32_t sq, int32_t* axis, uint32_t* index, uint32_t* pos) {
+    if (sq >= dev_err_n_) return fail(CDA_ERR_INVALID, "square index beyond the last device batch");
+    int rc;
+    if (order_used_ && order_ev_ && (rc = check(hipEventSynchronize(order_ev_), "hipEventSynchronize (last call)")))
+        return rc;
+    uint32_t w = 0xFFFFFFFFu;
+    if ((rc = check(hipMemcpyAsync(&w, dev_err_.as<uint32_t>() + sq, 4, hipMemcpyDeviceToHost, stream_),
+                    "hipMemcpyAsync push-order word")))
+        return rc;
+    if ((rc = check(hipStreamSynchronize(stream_), "hipStreamSynchronize"))) return rc;
+    if (w == 0xFFFFFFFFu) {
+        *axis = -1;
+        *index = *pos = 0;
+    } else {
+        *axis = (int32_t)(w >> 24);
+        *index = (w >> 12) & 0xFFF;
+        *pos = w & 0xFFF;
+    }
+    return CDA_OK;
+}
+
 // Build the reference's error text for the first violating square.
 int Engine::push_order_error(const uint32_t* err_words, uint32_t n, const uint8_t* src, uint32_t k,
                              bool src_is_eds) {
@@ -966,7 +992,7 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
     const size_t row = (size_t)k * kShare, W = 2 * (size_t)k;
     const size_t rows = (size_t)n * k;
     static const unsigned cap = [] {
-        const char* e = getenv("CDA_HOST_THREADS");
+        const char* e = deploy_knob("CDA_HOST_THREADS");
         const unsigned hw = std::thread::hardware_concurrency();
         unsigned v = e ? (unsigned)atoi(e) : 8u;
         if (hw && v > hw) v = hw;
@@ -976,7 +1002,7 @@ void Engine::copy_q0(const uint8_t* ods, uint32_t k, uint32_t n, uint8_t* eds) {
     // streaming stores (CDA_HOST_NT, default on): the EDS rows are not read
     // back here, so skip the read-for-ownership of every destination line
     static const bool nt_stores = [] {
-        const char* e = getenv("CDA_HOST_NT");
+        const char* e = test_knob("CDA_HOST_NT");
         return e ? atoi(e) != 0 : true;
     }();
     auto part = [&](unsigned t) {

@@ -18,6 +18,7 @@
 // once (4k^2 leaf hashes instead of the reference's 8k^2).  One thread per
 // leaf / per parent node; each NMT level of all 4k trees of every square in
 // the batch is one launch.  SHA-256 is pure 32-bit VALU work (no MFMA).
+#include "knobs.h"
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
@@ -1041,7 +1042,7 @@ hipError_t launch_row_order(const CellGrid& g, uint32_t n, uint32_t* err, hipStr
 static size_t hash_lds(const void* fn) {
     static long v = -2;
     if (v == -2) {
-        const char* e = getenv("CDA_HASH_LDS");
+        const char* e = test_knob("CDA_HASH_LDS");
         v = e ? atol(e) : 0;
     }
     if (v > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v);
@@ -1064,7 +1065,7 @@ static uint32_t device_cus() {
 // CDA_HASH_WG_PER_CU x the device's CUs (persistent; tuning / batch pipeline).
 static uint32_t hash_grid(uint32_t nblocks) {
     static const uint32_t cap = [] {
-        const char* e = getenv("CDA_HASH_WG_PER_CU");
+        const char* e = test_knob("CDA_HASH_WG_PER_CU");
         const int per = e ? atoi(e) : 0;
         return per > 0 ? (uint32_t)per * device_cus() : 0u;
     }();
@@ -1075,7 +1076,7 @@ static uint32_t hash_grid(uint32_t nblocks) {
 // runs (default 32 768 = half a wave per SIMD of one-lane cells; 0 = never).
 static uint64_t leaf_pair_max() {
     static const uint64_t v = [] {
-        const char* e = getenv("CDA_LEAF_PAIR_MAX");
+        const char* e = test_knob("CDA_LEAF_PAIR_MAX");
         return e ? strtoull(e, nullptr, 10) : 32768ull;
     }();
     return v;
@@ -1134,7 +1135,7 @@ hipError_t launch_subtrees(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
 // data root instead of the lane-pair compression.
 bool pair_sha_enabled() {
     static const bool v = [] {
-        const char* e = getenv("CDA_TOP_PAIR");
+        const char* e = test_knob("CDA_TOP_PAIR");
         return !(e && atoi(e) == 0);
     }();
     return v;
@@ -1144,7 +1145,7 @@ bool pair_sha_enabled() {
 // schedule helpers (CDA_DR_HELPERS=0: no helpers; CDA_TOP_PAIR=0: no pairs)
 static uint32_t data_root_mode() {
     static const bool dr_helpers = [] {
-        const char* e = getenv("CDA_DR_HELPERS");
+        const char* e = test_knob("CDA_DR_HELPERS");
         return !(e && atoi(e) == 0);
     }();
     return pair_sha_enabled() ? (dr_helpers ? 2u : 1u) : 0u;
@@ -1170,7 +1171,7 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
     if (dig && trees == n_items && (n_items & (n_items - 1)) == 0 && tpw <= n_items)
         while ((2u << lv) <= tpw && (n_items >> (lv + 1)) >= 2) lv++;
     static const bool rfc_in_top = [] {   // CDA_TOP_RFC=0: leaf digests only (A/B knob)
-        const char* e = getenv("CDA_TOP_RFC");
+        const char* e = test_knob("CDA_TOP_RFC");
         return !(e && atoi(e) == 0);
     }();
     if (!rfc_in_top) lv = 0;
@@ -1183,7 +1184,7 @@ hipError_t launch_tree_top(const Forest* f, uint32_t n_forest, uint32_t n_in, ui
     const dim3 grid((trees + tpw - 1) / tpw, n);
     // CDA_TOP_HELPERS=0 (A/B knob): no schedule-helper waves in the narrow levels
     static const uint32_t helpers = [] {
-        const char* e = getenv("CDA_TOP_HELPERS");
+        const char* e = test_knob("CDA_TOP_HELPERS");
         return e && atoi(e) == 0 ? 0u : kTopHelpers;
     }();
     if (pair)

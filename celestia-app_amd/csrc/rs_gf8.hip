@@ -18,6 +18,7 @@
 // GF(2^8) multiply by a constant c: the byte is cut into four 2-bit chunks,
 // each looked up in a 4-entry table dword with v_perm_b32(T, T, sel) -- 4 perms
 // (half rate), 7 selector ops, 2 XOR3 per 4 bytes; tables are immediates.
+#include "knobs.h"
 #include <cstdlib>
 
 #include "cda_kernels.h"
@@ -194,7 +195,7 @@ hipError_t launch_rs8_job(const RsJob& j, uint32_t k, uint32_t n, hipStream_t s)
     // k = 128: bitsliced encoder (rs_gf8_bs.hip) unless a segment is not a
     // multiple of its 4-codeword workgroup (or CDA_RS8_BYTEFORM=1 forces this
     // byte-form encoder, for A/B measurement).
-    static const bool byteform = getenv("CDA_RS8_BYTEFORM") && atoi(getenv("CDA_RS8_BYTEFORM"));
+    static const bool byteform = test_knob("CDA_RS8_BYTEFORM") && atoi(test_knob("CDA_RS8_BYTEFORM"));
     if (k == 128 && !byteform && j.seg[0].n_cw % 4 == 0 && (j.n_seg < 2 || j.seg[1].n_cw % 4 == 0))
         return launch_rs8_bs(j, n, s);
     switch (k) {

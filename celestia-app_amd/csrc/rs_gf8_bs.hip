@@ -20,6 +20,7 @@
 //   B->C    the inverse exchange;
 //   pass C  wave u: FFT d = 8..1, planes -> bytes, stores 16 parity shards.
 // 128 data VGPRs per lane, 2 waves per SIMD, 1 workgroup per CU.
+#include "knobs.h"
 #include "bitslice8.h"
 #include "cda_kernels.h"
 
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 // 2: the half-footprint variant; A/B knob).
 static int rs8_variant() {
     static const int v = [] {
-        const char* e = getenv("CDA_RS8_BS");
+        const char* e = test_knob("CDA_RS8_BS");
         return e ? atoi(e) : 2;
     }();
     return v;
@@ -337,7 +338,7 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
         // CDA_RS8_LDS (tuning): LDS reserved per workgroup, >= 64 KiB; above
         // 80 KiB one workgroup per CU, leaving VGPRs for co-running hash waves
         static const uint32_t lds = [] {
-            const char* e = getenv("CDA_RS8_LDS");
+            const char* e = test_knob("CDA_RS8_LDS");
             const uint32_t v = e ? (uint32_t)atoi(e) : 0;
             return v > kHalfLdsBytes && v <= 160 * 1024 ? v : kHalfLdsBytes;
         }();
@@ -355,13 +356,13 @@ hipError_t launch_rs8_bs(const RsJob& j, uint32_t n, hipStream_t s) {
         // (fewer than 2 per CU: one k = 128 square has 256 + 128) takes one
         // per workgroup (CDA_RS8_ONE=0/1 forces either, A/B knob)
         static const int one_env = [] {
-            const char* e = getenv("CDA_RS8_ONE");
+            const char* e = test_knob("CDA_RS8_ONE");
             return e ? atoi(e) : -1;
         }();
         const bool one = one_env >= 0 ? one_env != 0 : (uint64_t)ncw * n < 2u * 256u;
         // batches: XCD-aware 128-B slices (CDA_RS8_SLICE=0 turns them off, A/B knob)
         static const int slice_env = [] {
-            const char* e = getenv("CDA_RS8_SLICE");
+            const char* e = test_knob("CDA_RS8_SLICE");
             return e ? atoi(e) : 1;
         }();
         // only where two segments read the same bytes (the Q0 launch: rows

@@ -190,6 +190,13 @@ int cda_data_root(cda_ctx *ctx, const uint8_t *row_roots, const uint8_t *col_roo
 /* Details of the calling thread's last CDA_ERR_PUSH_ORDER: axis (0 row, 1
  * column), the axis index, and the leaf position whose push failed. */
 int cda_push_order_detail(cda_ctx *ctx, int32_t *axis, uint32_t *index, uint32_t *position);
+/* The same detail for square `square` of the context's last device batch
+ * (cda_extend_dah_device / cda_extend_dah_inplace_device), whose d_status
+ * carries only CDA_ERR_PUSH_ORDER: waits for that batch's GPU work, then
+ * decodes the square's first violation (axis -1 when the square is ordered).
+ * Valid until the next device batch on the context.  A block-replay caller
+ * (app/process_proposal.go:138-147) builds the rejection text from it. */
+int cda_push_order_detail_at(cda_ctx *ctx, uint32_t square, int32_t *axis, uint32_t *index, uint32_t *position);
 
 /* Config 5: ONE square split across G ranks (one GPU each), row blocks +
  * column blocks.  k = ODS width, W = 2k, R = k/G rows and C = W/G columns per
@@ -237,6 +244,9 @@ int cda_split_combine(cda_ctx *ctx, const void *d_row_subtree_slots, uint32_t pa
 int cda_comm_unique_id(uint8_t id[CDA_COMM_ID_BYTES]);
 int cda_comm_init(cda_ctx *ctx, int rank, int world, const uint8_t id[CDA_COMM_ID_BYTES]);
 int cda_comm_destroy(cda_ctx *ctx);
+/* The live communicator's rank and rank count as RCCL formed them
+ * (ncclCommUserRank / ncclCommCount); CDA_ERR_INVALID without one. */
+int cda_comm_size(cda_ctx *ctx, int *rank, int *world);
 /* ncclCommAbort of the context's communicator (then released).  Takes no
  * context lock, so a host watchdog may call it from another thread while a
  * call on the context waits in a collective for a peer that failed.  Errors

@@ -57,3 +57,44 @@ def test_no_oracle_in_product():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "coracle" not in txt and "pyref" not in txt and "liboracle" not in txt, f
+
+
+DEPLOY_KNOBS = {"CDA_SYNC_CHECK", "CDA_HOST_THREADS", "CDA_HOST_REGISTER", "CDA_HOST_PIPE_CHUNK",
+                "CDA_PIPELINE_CHUNK"}
+
+
+def test_product_library_reads_only_deploy_knobs():
+    """VERDICT r5, item 6 / ADVICE r5: libcda.so reads at most 10 environment
+    variables -- the deployer knobs of csrc/knobs.h -- and no test knob (fault
+    injection, A/B switches) is even named in it; the sources read the
+    environment only through knobs.h."""
+    assert len(DEPLOY_KNOBS) <= 10
+    import knobs
+    assert set(knobs.DEPLOY_KNOBS) == DEPLOY_KNOBS
+    blob = open(LIB, "rb").read()
+    named = set(m.decode() for m in re.findall(rb"CDA_[A-Z0-9_]+", blob))
+    assert named <= DEPLOY_KNOBS, sorted(named - DEPLOY_KNOBS)
+    csrc = os.path.join(ROOT, "celestia-app_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f == "knobs.h":
+            continue
+        txt = open(os.path.join(csrc, f)).read()
+        assert "getenv(" not in txt, f
+        for name in re.findall(r'deploy_knob\("(\w+)"\)', txt):
+            assert name in DEPLOY_KNOBS, (f, name)
+
+
+def test_test_build_is_separate():
+    """The test build (fault injection, A/B knobs) is its own library with its
+    own version string; the product library is not it."""
+    p = os.path.join(ROOT, "celestia-app_amd", "libcda_test.so")
+    if not os.path.exists(p):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "celestia-app_amd"), "-j8", "test-lib"])
+    t = ctypes.CDLL(p)
+    t.cda_version.restype = ctypes.c_char_p
+    assert t.cda_version().endswith(b"test-build")
+    blob = open(p, "rb").read()
+    assert b"CDA_FAULT" in blob and b"CDA_COMM_FAULT" in blob
+    prod = ctypes.CDLL(LIB)
+    prod.cda_version.restype = ctypes.c_char_p
+    assert not prod.cda_version().endswith(b"test-build")

@@ -16,6 +16,8 @@ import os
 
 import pytest
 
+import knobs
+
 pytestmark = pytest.mark.gpu
 
 
@@ -62,7 +64,7 @@ def comm_setup():
     k = 16
     dev = torch.device("cuda", 0)
     d_ods = torch.from_numpy(testfactory.random_square(k, 9)).to(dev)
-    c = _lib.Context(0)
+    c = _lib.Context(0, lib_path=knobs.lib_path_for_tests())   # CDA_COMM_FAULT: test build only
     c.comm_init(0, 1, _lib.comm_unique_id())
     yield c, d_ods, k
     os.environ.pop("CDA_COMM_FAULT", None)

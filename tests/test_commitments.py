@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import inclusion as oinc
+import knobs
 import square as osq
 from celestia_da import SquareError, blobfactory
 from celestia_da import inclusion as ginc
@@ -103,15 +104,19 @@ def test_commitments_blob_groups_gpu(ctx, ucap, fused, monkeypatch):
     wave (ucap 1000), including empty and one-share blobs; and the same
     batch through commitment_fused_kernel (subtree levels in LDS, the
     default for blobs of at most 512 shares)."""
-    monkeypatch.setenv("CDA_COMMIT_UCAP", ucap)
+    monkeypatch.setenv("CDA_COMMIT_UCAP", ucap)     # test knobs: read per call by the test build only
     monkeypatch.setenv("CDA_COMMIT_FUSED", fused)
+    tc = knobs.ctx_with({})
     rng = np.random.default_rng(21)
     sizes = [int(x) for x in rng.integers(1, 60_000, 150)] + [0, 1, 478, 0] + [int(x) for x in rng.integers(1, 900, 40)]
     blobs = random_blobs(21, sizes)
-    for threshold in (64, 2):
-        got = ginc.create_commitments(blobs, threshold)
-        for b, c in zip(blobs, got):
-            assert c == oinc.create_commitment(b.namespace, b.data, 0, threshold), (len(b.data), threshold)
+    try:
+        for threshold in (64, 2):
+            got = ginc.create_commitments(blobs, threshold, ctx=tc)
+            for b, c in zip(blobs, got):
+                assert c == oinc.create_commitment(b.namespace, b.data, 0, threshold), (len(b.data), threshold)
+    finally:
+        tc.close()
 
 
 @pytest.mark.gpu

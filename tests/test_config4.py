@@ -130,6 +130,84 @@ def test_config4_all_1024_squares_one_submission(ctx):
         assert _sha(eds[p].cpu().numpy()) == g["squares"][str(i)]["eds_sha256"], (p, i)
     assert list(bench.shard(0, 1, 1024)) == list(range(1024))
 
+    # Push-order status on this path: the same arena with
+    # Q0 namespace violations in the squares at positions 700 and 1023 (the
+    # one-hash-stream, 524 288-lane subtree schedule of >= 64 squares).  Only
+    # those statuses are set, cda_push_order_detail_at equals a brute-force
+    # first violation, and every other data root still equals the fixtures
+    # (app/process_proposal.go:138-147 rejects on exactly that status).
+    bad = {700: (40, 77), 1023: (127, 1)}
+    want_detail = {}
+    for p, (r0, c0) in bad.items():
+        q0 = eds[p, :k, :k].cpu().numpy()
+        q0[r0, c0, :29] = q0[0, 0, :29]
+        want_detail[p] = _first_violation(q0)
+        assert want_detail[p] is not None
+        eds[p, r0, c0, :29] = torch.from_numpy(q0[r0, c0, :29].copy()).to(dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert sorted(np.nonzero(st)[0].tolist()) == sorted(bad), np.nonzero(st)[0][:8]
+    assert all(st[p] == -3 for p in bad)      # CDA_ERR_PUSH_ORDER
+    for p in bad:
+        assert ctx.push_order_detail_at(p) == want_detail[p], p
+    assert ctx.push_order_detail_at(0) == (-1, 0, 0)
+    dr = roots.cpu().numpy()
+    diff = [p for p, i in enumerate(order) if p not in bad and dr[p].tobytes().hex() != g["squares"][str(i)]["data_root"]]
+    assert not diff, f"{len(diff)} ordered squares changed their data root, first {diff[:4]}"
+    with pytest.raises(Exception):
+        ctx.push_order_detail_at(n)            # beyond the last device batch
+
+
+def _first_violation(q0):
+    """Brute-force nmt push-order check of one Q0 (k x k x 512): the smallest
+    (axis, index, position) whose namespace is below its predecessor's (rows
+    before columns), as cda_push_order_detail reports."""
+    k = q0.shape[0]
+    ns = [[bytes(q0[r, c, :29]) for c in range(k)] for r in range(k)]
+    bad = [(0, r, c) for r in range(k) for c in range(1, k) if ns[r][c] < ns[r][c - 1]]
+    bad += [(1, c, r) for c in range(k) for r in range(1, k) if ns[r][c] < ns[r - 1][c]]
+    return min(bad) if bad else None
+
+
+@pytest.mark.gpu
+def test_push_order_status_k512_batch_of_two(ctx):
+    """Config 3's GF(2^16) path with a Q0 namespace violation in the second
+    square of a batch of 2 (in place): status [0, CDA_ERR_PUSH_ORDER], the
+    detail of square 1 equals a brute-force first violation, and square 0's
+    data root equals tests/golden/k512.json."""
+    import torch
+
+    from celestia_da import testfactory
+    with open(os.path.join(HERE, "golden", "k512.json")) as f:
+        g = json.load(f)["squares"]
+    k, n = 512, 2
+    W = 2 * k
+    dev = torch.device("cuda", 0)
+    q0 = testfactory.random_square(k, 0).reshape(k, k, 512)
+    bad = q0.copy()
+    bad[300, 5, :29] = bad[0, 0, :29]
+    bad[2, 400, :29] = bad[0, 0, :29]
+    want = _first_violation(bad)
+    assert want is not None
+    eds = torch.empty((n, W, W, 512), dtype=torch.uint8, device=dev)
+    eds[0, :k, :k] = torch.from_numpy(q0).to(dev)
+    eds[1, :k, :k] = torch.from_numpy(bad).to(dev)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert status.cpu().tolist() == [0, -3]
+    assert ctx.push_order_detail_at(1) == want
+    assert ctx.push_order_detail_at(0) == (-1, 0, 0)
+    assert roots[0].cpu().numpy().tobytes().hex() == g["0"]["data_root"]
+    del eds
+    torch.cuda.empty_cache()
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,rank", [(2, 1), (4, 2)])

@@ -111,3 +111,19 @@ def test_from_proto_six_roots_on_gpu(ctx):
     c = [bytes([0x80 + i]) * 90 for i in range(6)]
     d = da.data_availability_header_from_proto({"row_roots": r, "column_roots": c})
     assert d.hash() == pyref.merkle_root(r + c)
+
+
+def test_batch_shape_from_array_shape():
+    """da._batch_shape: k comes from the array's shape, never
+    rounded; an empty batch is (0, k); a non-square shape is an error."""
+    import numpy as np
+    from celestia_da import da as cda
+    assert cda._batch_shape(np.zeros((3, 64, 512), np.uint8)) == (3, 8)
+    assert cda._batch_shape(np.zeros((2, 16, 16, 512), np.uint8)) == (2, 16)
+    assert cda._batch_shape(np.zeros((0, 16, 512), np.uint8)) == (0, 4)
+    for bad in ((3, 60, 512), (2, 8, 4, 512), (2, 64, 256)):
+        try:
+            cda._batch_shape(np.zeros(bad, np.uint8))
+        except ValueError:
+            continue
+        raise AssertionError(bad)

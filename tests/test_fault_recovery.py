@@ -30,21 +30,13 @@ import pytest
 
 import coracle
 from celestia_da import CdaError, _lib, da
+import knobs
 
 pytestmark = pytest.mark.gpu
 
 
 def _ctx_with(env):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return _lib.Context(int(os.environ.get("CDA_DEVICE", "-1")))
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    return knobs.ctx_with(env)   # CDA_FAULT is read only by the test build (csrc/knobs.h)
 
 
 def _squares(k, n, seed):

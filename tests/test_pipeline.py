@@ -11,21 +11,13 @@ import pytest
 
 import coracle
 from celestia_da import _lib, da
+import knobs
 
 pytestmark = pytest.mark.gpu
 
 
 def _ctx_with(env):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return _lib.Context(int(os.environ.get("CDA_DEVICE", "-1")))
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    return knobs.ctx_with(env)   # A/B schedule knobs: the test build reads them (csrc/knobs.h)
 
 
 @pytest.mark.parametrize("k,n,env", [

@@ -19,6 +19,8 @@ import sys
 
 import pytest
 
+import knobs
+
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -55,6 +57,7 @@ print(json.dumps(out))
 def _run(env_extra: dict, k: int, n: int) -> list:
     env = dict(os.environ)
     env.update(env_extra)
+    env["CDA_LIB"] = knobs.lib_path_for_tests()   # the A/B knobs are read only by the test build
     r = subprocess.run([sys.executable, "-c", _CHILD, "x", str(k), str(n)], env=env, capture_output=True,
                        text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
