@@ -168,39 +168,17 @@ __device__ __forceinline__ uint32_t swap_h(uint32_t v) {   // lane l <- its shar
 //     Q0 launch's row and column passes then read each 128-B line of Q0 from
 //     the fabric once (the second read hits the XCD's L2) instead of twice.
 //     Speed only; correctness does not depend on the placement.
+// The codewords of one workgroup (every MODE): lane codeword cwb + lcw of
+// square sq, lane columns col..col+15 and col+kHi..col+kHi+15 (cwb uniform:
+// segments hold whole workgroups).  E: the exchange buffer (64 KiB of LDS).
 template <int MODE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job,
-                                                                                                   uint32_t nsq) {
+__device__ __forceinline__ void rs8_half_body(const RsJob& job, uint32_t* E, uint32_t sq, uint32_t cwb, uint32_t lcw,
+                                              uint32_t col) {
     constexpr bool ONE = MODE == 1;
-    extern __shared__ uint32_t E[];
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t l = threadIdx.x & 63;
     const uint32_t h = MODE == 2 ? (l >> 2) & 1 : (l >> 4) & 1;
     const uint32_t h0 = h ? 0u : 0xFFFFFFFFu;
-    // cwb: the workgroup's first codeword (uniform: segments hold whole
-    // workgroups), lane codeword cwb + lcw, lane columns col..col+15 and
-    // col+kHi..col+kHi+15
-    uint32_t sq, cwb, lcw, col;
-    if constexpr (MODE == 2) {
-        // grid: groups of 8 units x P workgroups, unit u's j-th workgroup at
-        // block 8P*(u/8) + 8j + u%8
-        const uint32_t ncw = job.seg[0].n_cw + (job.n_seg > 1 ? job.seg[1].n_cw : 0);
-        const uint32_t P = ncw / 8;
-        const uint32_t b = blockIdx.x, grp = b / (8 * P), r = b % (8 * P);
-        const uint32_t unit = grp * 8 + (r & 7), j = r >> 3;
-        sq = unit >> 2;
-        if (sq >= nsq) return;   // the last group's missing units
-        cwb = 8 * j;
-        lcw = l >> 3;
-        col = 128 * (unit & 3) + 16 * (l & 3);
-        if (job.err_init && (unit & 3) == 0 && j == 0 && threadIdx.x == 0) job.err_init[sq] = 0xFFFFFFFFu;
-    } else {
-        rs_err_init(job);
-        sq = blockIdx.y;
-        cwb = ONE ? blockIdx.x : 2 * blockIdx.x;
-        lcw = ONE ? 0u : l >> 5;
-        col = 16 * (l & 15);
-    }
     const bool s1 = job.n_seg > 1 && cwb >= job.seg[0].n_cw;
     const RsSeg& g = s1 ? job.seg[1] : job.seg[0];
     const bool live = !ONE || l < 32;
@@ -315,6 +293,38 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                 make_uint4(R[8 * j + 4], R[8 * j + 5], R[8 * j + 6], R[8 * j + 7]);
         }
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void rs8_bs_half_kernel(const RsJob job,
+                                                                                                   uint32_t nsq) {
+    constexpr bool ONE = MODE == 1;
+    extern __shared__ uint32_t E[];
+    const uint32_t l = threadIdx.x & 63;
+    // cwb: the workgroup's first codeword, lane codeword cwb + lcw, lane
+    // columns col..col+15 and col+kHi..col+kHi+15
+    uint32_t sq, cwb, lcw, col;
+    if constexpr (MODE == 2) {
+        // grid: groups of 8 units x P workgroups, unit u's j-th workgroup at
+        // block 8P*(u/8) + 8j + u%8
+        const uint32_t ncw = job.seg[0].n_cw + (job.n_seg > 1 ? job.seg[1].n_cw : 0);
+        const uint32_t P = ncw / 8;
+        const uint32_t b = blockIdx.x, grp = b / (8 * P), r = b % (8 * P);
+        const uint32_t unit = grp * 8 + (r & 7), j = r >> 3;
+        sq = unit >> 2;
+        if (sq >= nsq) return;   // the last group's missing units
+        cwb = 8 * j;
+        lcw = l >> 3;
+        col = 128 * (unit & 3) + 16 * (l & 3);
+        if (job.err_init && (unit & 3) == 0 && j == 0 && threadIdx.x == 0) job.err_init[sq] = 0xFFFFFFFFu;
+    } else {
+        rs_err_init(job);
+        sq = blockIdx.y;
+        cwb = ONE ? blockIdx.x : 2 * blockIdx.x;
+        lcw = ONE ? 0u : l >> 5;
+        col = 16 * (l & 15);
+    }
+    rs8_half_body<MODE>(job, E, sq, cwb, lcw, col);
 }
 
 }  // namespace

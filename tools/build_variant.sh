@@ -19,7 +19,8 @@ if [ -n "$PATCH" ]; then
   patch -s -d $T/pkg -p1 < "$PATCH"
   PKG=$T/pkg
 fi
-make -C $PKG -j8 BUILD=$OUT/obj LIB=$OUT/libcda.so HIPFLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $*" >/dev/null
+# -DCDA_TESTING: a variant is a test build, so the A/B knobs (csrc/knobs.h) still apply to it
+make -C $PKG -j8 BUILD=$OUT/obj LIB=$OUT/libcda.so HIPFLAGS="-O3 -std=c++20 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -DCDA_TESTING $*" >/dev/null
 rm -rf $OUT/obj   # objects stay local: only the library travels to the GPU box
 [ -n "$PATCH" ] && rm -rf "$T"
 echo $OUT/libcda.so
