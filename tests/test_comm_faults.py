@@ -72,6 +72,19 @@ def comm_setup():
     c.close()
 
 
+def test_comm_size_reports_the_communicator(ctx, comm_setup):
+    """cda_comm_size: the rank and rank count RCCL formed (what bench.py
+    reports as config 5's communicator_ranks); no communicator -> error."""
+    from celestia_da import CdaError, _lib
+    c, _, _ = comm_setup
+    assert c.comm_size() == (0, 1)
+    c.comm_destroy()
+    with pytest.raises(CdaError, match="cda_comm_init"):
+        c.comm_size()
+    c.comm_init(0, 1, _lib.comm_unique_id())
+    assert c.comm_size() == (0, 1)
+
+
 @pytest.mark.parametrize("where", ["gather", "a2a_or_gather"])
 def test_rccl_failure_closes_group_aborts_and_recovers(ctx, comm_setup, where):
     """A failed RCCL call inside a group: CDA_ERR_COMM, the communicator is
