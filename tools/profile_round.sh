@@ -1,15 +1,9 @@
 #!/bin/bash
-# Collect the rocprofv3 evidence for one round on a GPU box (run via gpurun).
-# Usage: tools/profile_round.sh <tag>   -> gpurun_out/prof_<tag>/...
+# A round's evidence in one GPU call: the GPU suite, smoke() and the default
+# bench (tools/run_round.sh), then the fixed-shape kernel traces + PMC passes
+# of tools/profile_round3.sh (k = 128: config 4's 1024 squares per step;
+# k = 512: one square per step).  Usage: bash tools/profile_round.sh <tag>
 set -o pipefail
-TAG=${1:-r01}
-OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
-mkdir -p $OUT
-cd /tmp
-export TMPDIR=/tmp
-B="$GRAFT_REPO_ROOT/bench.py --no-cpu --no-extras"
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $B > $OUT/fetch.log 2>&1 || exit 2
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $B > $OUT/write.log 2>&1 || exit 3
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- python3 $B > $OUT/sq.log 2>&1 || exit 4
-echo done
+TAG=${1:?tag}
+bash tools/run_round.sh "$TAG" || exit $?
+bash tools/profile_round3.sh "$TAG" > "gpurun_out/$TAG/profile.log" 2>&1
