@@ -844,6 +844,18 @@ def blob_commitments(ctx, dev, stream, n_blocks: int = 64, reps: int = 10) -> di
             "workload": f"all blobs of {n_blocks} full k=128 blocks (CheckTx/ProcessProposal ValidateBlobTx)"}
 
 
+def gather_parity(parity: dict, world: int, device) -> dict:
+    """Every rank's {checked, matched} fixture counts, summed, with the
+    per-rank list (rank order) -- what rank 0's line reports at N > 1."""
+    import torch
+    import torch.distributed as dist
+    pt = torch.tensor([parity["checked"], parity["matched"]], dtype=torch.int64, device=device)
+    allp = [torch.zeros_like(pt) for _ in range(world)]
+    dist.all_gather(allp, pt)
+    per = [[int(x[0]), int(x[1])] for x in allp]
+    return {"checked": sum(c for c, _ in per), "matched": sum(m for _, m in per), "per_rank": per}
+
+
 def launch_mode(gpus: int, env) -> str:
     """How `bench.py --gpus N` runs:
     - WORLD_SIZE set (torch.distributed.run or our own spawn): this process is
@@ -1058,12 +1070,7 @@ def main():
         return float(t.item())
 
     if world > 1:   # every rank's shard is checked against the fixture; the line reports all of them
-        pt = torch.tensor([parity["checked"], parity["matched"]], dtype=torch.int64,
-                          device=dev if dist.get_backend() == "nccl" else "cpu")
-        allp = [torch.zeros_like(pt) for _ in range(world)]
-        dist.all_gather(allp, pt)
-        per = [[int(x[0]), int(x[1])] for x in allp]
-        parity = {"checked": sum(c for c, _ in per), "matched": sum(m for _, m in per), "per_rank": per}
+        parity = gather_parity(parity, world, dev if dist.get_backend() == "nccl" else "cpu")
 
     # the timed region runs the product path exactly as a caller would (no
     # stage events); the per-stage HIP-event breakdown comes from a separate

@@ -72,3 +72,31 @@ def test_spawn_propagates_rank_failure():
 @pytest.mark.parametrize("rc,want", [(1, 1), (2, 2), (-9, 137), (-6, 134)])
 def test_exit_status(rc, want):
     assert bench._exit_status(rc) == want
+
+
+def _parity_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = bench.gather_parity({"checked": 10 + rank, "matched": 10 + rank - (rank == 1)}, world, "cpu")
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_gather_parity_gloo():
+    """Rank 0's line sums every rank's fixture checks and lists them per rank
+    (world size 3 over gloo; rank 1 reports one mismatch)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    procs = [ctx.Process(target=_parity_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {"checked": 33, "matched": 32, "per_rank": [[10, 10], [11, 10], [12, 12]]}
+    assert all(res[r] == want for r in range(3))
