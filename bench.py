@@ -906,9 +906,28 @@ def spawn_ranks(argv: list, gpus: int, grace_s: float = 60.0) -> int:
     groups are killed.  Returns the first non-zero exit status, else 0."""
     import signal
     import subprocess
+
+    def die_with_parent():   # in the child, before exec: SIGKILL when this parent dies, however it dies
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+
     procs = []
+
+    def forward(signum, frame):   # a launcher's SIGTERM / ^C reaches every rank's process group
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
     for cmd, env in rank_commands(argv, gpus, free_port(), os.environ):
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+        # own session per rank: a failed run kills each rank's whole subtree
+        # (its config-5 child too) with one killpg
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True, preexec_fn=die_with_parent))
     rc, failed_at = 0, None
     try:
         while any(p.poll() is None for p in procs):

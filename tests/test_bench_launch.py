@@ -100,3 +100,37 @@ def test_gather_parity_gloo():
         assert p.exitcode == 0
     want = {"checked": 33, "matched": 32, "per_rank": [[10, 10], [11, 10], [12, 12]]}
     assert all(res[r] == want for r in range(3))
+
+
+def test_parent_sigterm_kills_ranks(tmp_path):
+    """A launcher's SIGTERM to the GPU-free parent must take the rank
+    processes down with it (no orphaned ranks holding a GPU)."""
+    import signal
+    import time
+    script = tmp_path / "fake_rank.py"
+    script.write_text("import os, time\nopen(os.environ['PIDFILE'] + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+                      "time.sleep(60)\n")
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench\n"
+            f"bench.rank_commands = lambda argv, g, port, env: [([sys.executable, {str(script)!r}], "
+            f"dict(env, RANK=str(r))) for r in range(g)]\n"
+            f"sys.exit(bench.spawn_ranks([], 2))\n")
+    env = _env(PIDFILE=str(tmp_path / "pid"))
+    p = subprocess.Popen([sys.executable, "-c", code], env=env)
+    pids = []
+    for _ in range(100):
+        time.sleep(0.1)
+        files = [tmp_path / f"pid{r}" for r in range(2)]
+        if all(f.exists() and f.read_text() for f in files):
+            pids = [int(f.read_text()) for f in files]
+            break
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    time.sleep(0.5)
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = open(f"/proc/{pid}/stat").read().split()[2] != "Z"
+        except (ProcessLookupError, FileNotFoundError):
+            alive = False
+        assert not alive, pid
