@@ -224,10 +224,11 @@ int cda_extend_dah_device(cda_ctx* ctx, const void* d_ods, uint32_t k, uint32_t 
             return e.fail(CDA_ERR_INVALID, "null buffer");
         uint32_t* err = e.err_words(n);
         if (!err) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
-        e.set_device_batch(n);
-        return e.enqueue_extend_dah(static_cast<const uint8_t*>(d_ods), k, n, static_cast<uint8_t*>(d_eds),
-                                    static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
-                                    static_cast<uint8_t*>(d_data_roots), err, d_status, s);
+        const int rc = e.enqueue_extend_dah(static_cast<const uint8_t*>(d_ods), k, n, static_cast<uint8_t*>(d_eds),
+                                            static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
+                                            static_cast<uint8_t*>(d_data_roots), err, d_status, s);
+        e.set_device_batch(rc == CDA_OK ? n : 0);
+        return rc;
     });
 }
 
@@ -246,10 +247,11 @@ int cda_extend_dah_inplace_device(cda_ctx* ctx, uint32_t k, uint32_t n, void* d_
         if (!d_eds || !d_row_roots || !d_col_roots || !d_data_roots) return e.fail(CDA_ERR_INVALID, "null buffer");
         uint32_t* err = e.err_words(n);
         if (!err) return e.fail(CDA_ERR_OOM, "hipMalloc err words");
-        e.set_device_batch(n);
-        return e.enqueue_extend_dah(nullptr, k, n, static_cast<uint8_t*>(d_eds), static_cast<uint8_t*>(d_row_roots),
-                                    static_cast<uint8_t*>(d_col_roots), static_cast<uint8_t*>(d_data_roots), err,
-                                    d_status, s);
+        const int rc = e.enqueue_extend_dah(nullptr, k, n, static_cast<uint8_t*>(d_eds),
+                                            static_cast<uint8_t*>(d_row_roots), static_cast<uint8_t*>(d_col_roots),
+                                            static_cast<uint8_t*>(d_data_roots), err, d_status, s);
+        e.set_device_batch(rc == CDA_OK ? n : 0);
+        return rc;
     });
 }
 

@@ -159,10 +159,19 @@ class Engine {
     }
     // n push-order error words of a device entry point (context scratch), or
     // NULL when the allocation fails.
-    uint32_t* err_words(uint32_t n) { return dev_err_.ensure((size_t)n * 4) == hipSuccess ? dev_err_.as<uint32_t>() : nullptr; }
+    uint32_t* err_words(uint32_t n) {
+        void* before = dev_err_.ptr;
+        if (dev_err_.ensure((size_t)n * 4) != hipSuccess) {
+            dev_err_n_ = 0;
+            return nullptr;
+        }
+        if (dev_err_.ptr != before) dev_err_n_ = 0;   // a regrown buffer holds no batch's words
+        return dev_err_.as<uint32_t>();
+    }
     // The push-order words belong to the last device batch of n squares
     // (cda_extend_dah_device / _inplace_device): device_push_order_detail
     // reads square sq's word after that batch's work completed.
+    // n = 0: the last device batch failed to enqueue (no words to read)
     void set_device_batch(uint32_t n) { dev_err_n_ = n; }
     int device_push_order_detail(uint32_t sq, int32_t* axis, uint32_t* index, uint32_t* pos);
 

@@ -574,3 +574,44 @@ def test_threads_and_streams_on_one_context(ctx):
             assert np.array_equal(jb["r"][i].cpu().numpy().reshape(W, 90), e_rows), (jb["k"], i)
             assert np.array_equal(jb["c"][i].cpu().numpy().reshape(W, 90), e_cols), (jb["k"], i)
             assert jb["g"][i].cpu().numpy().tobytes() == e_root, (jb["k"], i)
+
+
+@pytest.mark.parametrize("k,n,bad", [(64, 9, (0, 4, 8)), (128, 5, (3,)), (256, 3, (1, 2))])
+def test_push_order_detail_at_every_square(ctx, k, n, bad):
+    """cda_push_order_detail_at after an in-place device batch: the squares in
+    `bad` carry a Q0 namespace violation (two of them at k = 256, on the
+    GF(2^16) path; k = 64 / 128 batches of < 64 squares hash on two streams),
+    each reports the brute-force first violation, every other square (-1, 0,
+    0) with its oracle data root; a square index past the batch is an error."""
+    import torch
+    from celestia_da import CdaError
+    W = 2 * k
+    dev = torch.device("cuda", 0)
+    sq = [coracle.random_square(k, 500 + i).reshape(k, k, 512).copy() for i in range(n)]
+    want = {}
+    for j, i in enumerate(bad):
+        r, c = (7 * j + 3) % k, (5 * j + 11) % k
+        if c == 0:
+            c = 1
+        sq[i][r, c, :29] = sq[i][0, 0, :29]
+        want[i] = _first_violation(sq[i])
+        assert want[i] is not None
+    eds = torch.zeros((n, W, W, 512), dtype=torch.uint8, device=dev)
+    for i in range(n):
+        eds[i, :k, :k] = torch.from_numpy(sq[i]).to(dev)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    st = status.cpu().tolist()
+    for i in range(n):
+        if i in want:
+            assert st[i] == -3 and ctx.push_order_detail_at(i) == want[i], i
+        else:
+            assert st[i] == 0 and ctx.push_order_detail_at(i) == (-1, 0, 0), i
+            assert bytes(roots[i].cpu().numpy()) == coracle.extend_dah(sq[i].reshape(-1, 512))[3], i
+    with pytest.raises(CdaError, match="last device batch"):
+        ctx.push_order_detail_at(n)
