@@ -13,6 +13,7 @@
 //                 stores W bytes to the same offset of Q1, Q2 and Q3
 //   line_rw     : the same bytes moved by 128-B-slice workgroups (the current
 //                 MODE-2 access shape: 4 lanes x 32 B per line) -- the baseline
+//   line_rw16   : the same, 8 lanes x 16 B per line (a whole line per load)
 // Prints per kernel: ms per N squares, algorithmic TB/s (32 MiB per square).
 #include <hip/hip_runtime.h>
 
@@ -117,6 +118,37 @@ __global__ __launch_bounds__(512) void line_rw(uint8_t* __restrict__ eds, uint32
     }
 }
 
+// the same bytes with 8 lanes x 16 B per 128-B line per instruction (a whole
+// line per 8 lanes, 2 lines per lane pair of instructions): lane l covers
+// 16 B at 16 (l % 8) of the slice's line for 2 cells per load pair
+__global__ __launch_bounds__(512) void line_rw16(uint8_t* __restrict__ eds, uint32_t nsq) {
+    const uint32_t b = blockIdx.x, x = b % 8, j = b / 8;
+    const uint32_t per = 4 * 16;
+    const uint32_t sq = 8 * (j / per) + x, rem = j % per, s = rem / 16, blk = rem % 16;
+    if (sq >= nsq) return;
+    uint8_t* base = eds + (size_t)sq * SQ + (size_t)s * 128 + 16 * (threadIdx.x & 7);
+    uint4 v[16];   // 16 cells per thread x 16 B
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t cell = blk * 1024 + i * 64 + (threadIdx.x >> 3);   // 1024 cells per workgroup
+        const uint32_t r = cell / K, c = cell % K;
+        v[i] = *reinterpret_cast<const uint4*>(base + ((size_t)r * Wd + c) * SH);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc ^= fold(v[i]);
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+        const uint32_t r0 = q & 2 ? K : 0, c0 = q & 1 ? K : 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t cell = blk * 1024 + i * 64 + (threadIdx.x >> 3);
+            const uint32_t r = cell / K + r0, c = cell % K + c0;
+            *reinterpret_cast<uint4*>(base + ((size_t)r * Wd + c) * SH) = mix(v[i], acc + q);
+        }
+    }
+}
+
 template <typename F>
 static float time_ms(F launch, int reps) {
     hipEvent_t a, b;
@@ -150,6 +182,8 @@ int main(int argc, char** argv) {
     };
     const uint32_t g = (n + 7) / 8 * 8;
     report("line_rw", time_ms([&] { hipLaunchKernelGGL(line_rw, dim3(g * 64), dim3(512), 0, 0, eds, n); }, 10));
+    report("line_rw16", time_ms([&] { hipLaunchKernelGGL(line_rw16, dim3(g * 64), dim3(512), 0, 0, eds, n); }, 10));
+    report("line_rw_b", time_ms([&] { hipLaunchKernelGGL(line_rw, dim3(g * 64), dim3(512), 0, 0, eds, n); }, 10));
     report("slice_rw16", time_ms([&] { hipLaunchKernelGGL(slice_rw<16>, dim3(g * 32), dim3(512), 0, 0, eds, n); }, 10));
     report("slice_rw8", time_ms([&] { hipLaunchKernelGGL(slice_rw<8>, dim3(g * 64), dim3(512), 0, 0, eds, n); }, 10));
     report("slice_rw4", time_ms([&] { hipLaunchKernelGGL(slice_rw<4>, dim3(g * 128), dim3(512), 0, 0, eds, n); }, 10));
