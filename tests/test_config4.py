@@ -360,3 +360,38 @@ def test_stage_report_is_per_step():
     assert r["nmt_levels"]["avg_ms"] == 1.0 and r["nmt_leaves"]["avg_ms"] == 1.5
     want = bench.compressions(512)["nmt_levels"] / 1e-3
     assert abs(r["nmt_levels"]["compressions_per_s"] - want) < 1e-6 * want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 7, 63, 64, 65])
+def test_inplace_batch_sizes_around_schedule_switches(ctx, n):
+    """Batch sizes on both sides of the engine's schedule switches -- one
+    codeword per RS workgroup below two per CU (a single square), the XCD-slice
+    Q0 launch, the two-stream hash split below 64 squares and one stream from
+    64 -- each against the oracle fixture (squares 0..n-1)."""
+    import torch
+
+    from celestia_da import testfactory
+    g = _fixture()["squares"]
+    k = 128
+    W = 2 * k
+    dev = torch.device("cuda", 0)
+    eds = torch.empty((n, W, W, 512), dtype=torch.uint8, device=dev)
+    for j0, part in testfactory.random_squares(k, list(range(n))):
+        eds[j0:j0 + part.shape[0], :k, :k] = torch.from_numpy(part).to(dev).view(-1, k, k, 512)
+    rows = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    cols = torch.empty(n, W * 90, dtype=torch.uint8, device=dev)
+    roots = torch.empty(n, 32, dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.extend_dah_inplace_device(k, n, eds.data_ptr(), rows.data_ptr(), cols.data_ptr(), roots.data_ptr(),
+                                  status.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    r, c, dr = rows.cpu().numpy(), cols.cpu().numpy(), roots.cpu().numpy()
+    for i in range(n):
+        assert dr[i].tobytes().hex() == g[str(i)]["data_root"], i
+        assert _sha(r[i].reshape(W, 90)) == g[str(i)]["row_roots_sha256"], i
+        assert _sha(c[i].reshape(W, 90)) == g[str(i)]["col_roots_sha256"], i
+    for i in {0, n - 1}:
+        if "eds_sha256" in g[str(i)]:
+            assert _sha(eds[i].cpu().numpy()) == g[str(i)]["eds_sha256"], i
