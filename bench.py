@@ -2,9 +2,13 @@
 """Benchmark: EDS+DAH squares/s on MI355X (BASELINE.json metric).
 
 One step = the whole hot path (ODS -> EDS -> 4k NMT roots -> data root) over
-one batch of `--batch` random-namespace k x k squares per rank, inputs already
-resident in HBM (cda_extend_dah_device).  Ranks shard independent squares (no
-collective on the data path: SURVEY.md 8(e), config 4) -> "scaling": "weak".
+config 4's fixed batch of 1 024 random-namespace k = 128 squares split over
+the ranks (rank g: squares [g*1024/N, (g+1)*1024/N); `--batch` overrides the
+per-rank count), inputs already resident in HBM, ODS in Q0 of the EDS arena
+(cda_extend_dah_inplace_device).  No collective on the data path (SURVEY.md
+8(e)); the total work is fixed as N grows -> "scaling": "strong".  N > 1:
+under torch.distributed.run, or `--gpus N` alone (this script then starts the
+N rank processes itself; launch_mode / spawn_ranks).
 Timing: W untimed steps, then K steps bracketed by barrier + synchronize, max
 over ranks.  Rank 0 prints one JSON line.
 
