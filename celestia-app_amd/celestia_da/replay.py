@@ -42,16 +42,28 @@ class BlockResult:
     accepted: bool | None = None      # data_root == expected DataHash (when given)
 
 
+def _layout_k(ctx_h, lib, buf, off, n, max_square_size, threshold):
+    """Square size of one flat block via cda_square_layout (host only); raises
+    SquareError with go-square's message."""
+    k = C.c_uint32()
+    rc = lib.cda_square_layout(ctx_h, ptr(buf), _u64p(off), n, max_square_size, threshold,
+                               _lib.CDA_SQUARE_CONSTRUCT, C.byref(k), None, None, None, 0, None)
+    if rc != _lib.CDA_OK:
+        msg = lib.cda_last_error(ctx_h).decode()
+        raise (_lib.SquareError if rc == _lib.CDA_ERR_SQUARE else _lib.CdaError)(rc, msg)
+    return k.value
+
+
 def plan(blocks, max_square_size: int = SQUARE_SIZE_UPPER_BOUND,
          subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD):
     """Host-only layout of every block: (square sizes, errors).  A block whose
     txs go-square rejects gets size 0 and the reference's message."""
-    from .square import layout
+    L = _lib.load()
     sizes, errors = [], []
     for txs in blocks:
+        buf, off = _flatten(txs)
         try:
-            k, _, _ = layout(txs, max_square_size, subtree_root_threshold)
-            sizes.append(k)
+            sizes.append(_layout_k(None, L, buf, off, len(txs), max_square_size, subtree_root_threshold))
             errors.append(None)
         except _lib.SquareError as e:
             sizes.append(0)
@@ -78,31 +90,64 @@ def _push_order_message(ods_sq: np.ndarray, k: int, detail) -> str:
             f"{bytes(cell(pos - 1)[:29]).hex()}, pushed: {bytes(cell(pos)[:29]).hex()}")
 
 
+def _stage_txs(blocks):
+    """Every block's txs in ONE page-locked host buffer (one copy of the
+    bytes), each block at a 16-byte aligned offset with >= 16 readable bytes
+    after it (cda_square_construct_device reads whole 16-B words): (pinned
+    uint8 tensor, its numpy view, [(start, tx offsets)] per block)."""
+    import torch
+    lay, pos = [], 0
+    for txs in blocks:
+        off = np.zeros(len(txs) + 1, dtype=np.uint64)
+        np.cumsum(np.fromiter(map(len, txs), dtype=np.uint64, count=len(txs)), out=off[1:])
+        lay.append((pos, off))
+        pos += (int(off[-1]) + 16 + 15) & ~15
+    pinned = torch.empty(max(pos, 16), dtype=torch.uint8, pin_memory=True)
+    host = pinned.numpy()
+    for txs, (start, off) in zip(blocks, lay):
+        n = int(off[-1])
+        if n:
+            np.concatenate([np.frombuffer(t, dtype=np.uint8) for t in txs], out=host[start:start + n])
+        host[start + n:start + n + 16] = 0
+    return pinned, host, lay
+
+
 def replay(blocks, data_hashes=None, max_square_size: int = SQUARE_SIZE_UPPER_BOUND,
-           subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD, ctx=None, device=None):
+           subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD, ctx=None, device=None, max_batch: int = 1024):
     """ProcessProposal's DA check for every block of `blocks` (each a list of
     tx bytes, in block order).  `data_hashes` (optional): the headers'
-    DataHash per block.  Returns one BlockResult per block."""
+    DataHash per block.  Blocks of one square size go to the GPU in batches
+    of at most `max_batch` squares (config 4's 1 024 at k = 128: 40 GiB of
+    ODS + EDS).  Returns one BlockResult per block."""
     import torch
     ctx = ctx or default_context()
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    sizes, errors = plan(blocks, max_square_size, subtree_root_threshold)
-    out = [BlockResult(square_size=k, error=e) for k, e in zip(sizes, errors)]
-    for k, idx in group_by_size(sizes).items():
+    pinned, host, lay = _stage_txs(blocks)
+    out = []
+    for txs, (start, off) in zip(blocks, lay):
+        seg = host[start:start + int(off[-1]) + 1]
+        try:
+            out.append(BlockResult(square_size=_layout_k(ctx.h, ctx.lib, seg, off, len(txs), max_square_size,
+                                                         subtree_root_threshold)))
+        except _lib.SquareError as e:
+            out.append(BlockResult(error=str(e)))
+    d_txs = torch.empty(pinned.numel(), dtype=torch.uint8, device=dev)
+    d_txs.copy_(pinned, non_blocking=True)       # one H2D of every block's txs
+    base = d_txs.data_ptr()
+    batches = [(k, idx[c:c + max_batch]) for k, idx in group_by_size([r.square_size for r in out]).items()
+               for c in range(0, len(idx), max_batch)]
+    for k, idx in batches:
         n, W = len(idx), 2 * k
         d_ods = torch.empty((n, k * k, SHARE_SIZE), dtype=torch.uint8, device=dev)
         for j, i in enumerate(idx):
-            buf, off = _flatten(blocks[i])
-            d_txs = torch.zeros(buf.size + 16, dtype=torch.uint8, device=dev)   # >= 16 B readable slack
-            d_txs[:buf.size].copy_(torch.from_numpy(buf))
+            start, off = lay[i]
+            seg = host[start:start + int(off[-1]) + 1]
             kk = C.c_uint32()
-            kept = (C.c_uint32 * max(1, len(blocks[i])))()
-            n_kept = C.c_uint32()
             ctx.check(ctx.lib.cda_square_construct_device(
-                ctx.h, ptr(buf), _u64p(off), len(blocks[i]), d_txs.data_ptr(), max_square_size,
+                ctx.h, ptr(seg), _u64p(off), len(blocks[i]), base + start, max_square_size,
                 subtree_root_threshold, _lib.CDA_SQUARE_CONSTRUCT, d_ods[j].data_ptr(), k * k * SHARE_SIZE,
-                C.byref(kk), kept, C.byref(n_kept), stream))
+                C.byref(kk), None, None, stream))
             assert kk.value == k, (i, kk.value, k)
         d_eds = torch.empty((n, W * W * SHARE_SIZE), dtype=torch.uint8, device=dev)
         rows = torch.empty((n, W * 90), dtype=torch.uint8, device=dev)
@@ -111,14 +156,14 @@ def replay(blocks, data_hashes=None, max_square_size: int = SQUARE_SIZE_UPPER_BO
         status = torch.empty(n, dtype=torch.int32, device=dev)
         ctx.extend_dah_device(d_ods.data_ptr(), k, n, d_eds.data_ptr(), rows.data_ptr(), cols.data_ptr(),
                               roots.data_ptr(), status.data_ptr(), stream)
-        torch.cuda.synchronize(dev)
-        st, rt = status.cpu().numpy(), roots.cpu().numpy()
+        st, rt = status.cpu().numpy(), roots.cpu().numpy()    # synchronises the stream
         for j, i in enumerate(idx):
             if st[j] == _lib.CDA_OK:
                 out[i].data_root = rt[j].tobytes()
             else:
                 out[i].error = _push_order_message(d_ods[j].cpu().numpy(), k, ctx.push_order_detail_at(j))
         del d_ods, d_eds
+    torch.cuda.current_stream(dev).synchronize()   # the pinned staging outlives every read of it
     if data_hashes is not None:
         for r, h in zip(out, data_hashes):
             r.accepted = r.error is None and r.data_root == bytes(h)

@@ -35,10 +35,15 @@ class Square(list):
 
 
 def _flatten(txs):
+    """One flat, writable tx buffer (never empty: a trailing 0 byte) and the
+    n + 1 offsets.  One copy of the bytes: np.concatenate of views for blocks
+    of few (large) txs, bytes.join for many small ones (per-item cost)."""
     off = np.zeros(len(txs) + 1, dtype=np.uint64)
-    for i, t in enumerate(txs):
-        off[i + 1] = off[i] + len(t)
-    buf = np.frombuffer(b"".join(txs) + b"\0", dtype=np.uint8).copy()   # never empty
+    np.cumsum(np.fromiter(map(len, txs), dtype=np.uint64, count=len(txs)), out=off[1:])
+    if len(txs) <= 512:
+        buf = np.concatenate([np.frombuffer(t, dtype=np.uint8) for t in txs] + [np.zeros(1, dtype=np.uint8)])
+    else:
+        buf = np.frombuffer(bytearray(b"".join(list(txs) + [b"\0"])), dtype=np.uint8)
     return buf, off
 
 

@@ -96,3 +96,6 @@ def test_replay_many_same_size(ctx):
     assert {r.square_size for r in res} == {32}
     for b, r in zip(blocks[::5], res[::5]):
         assert r.data_root == gsq.construct_extend_dah(b, 32, ctx=ctx)[4]
+    # the same blocks in batches of at most 7 squares (4 batches, the last ragged)
+    chunked = replay.replay(blocks, max_square_size=32, ctx=ctx, max_batch=7)
+    assert [r.data_root for r in chunked] == [r.data_root for r in res]
