@@ -113,15 +113,36 @@ def _stage_txs(blocks):
 
 
 def replay(blocks, data_hashes=None, max_square_size: int = SQUARE_SIZE_UPPER_BOUND,
-           subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD, ctx=None, device=None, max_batch: int = 1024):
+           subtree_root_threshold: int = SUBTREE_ROOT_THRESHOLD, ctx=None, device=None, max_batch: int = 1024,
+           max_stage_bytes: int = 1 << 31):
     """ProcessProposal's DA check for every block of `blocks` (each a list of
     tx bytes, in block order).  `data_hashes` (optional): the headers'
     DataHash per block.  Blocks of one square size go to the GPU in batches
     of at most `max_batch` squares (config 4's 1 024 at k = 128: 40 GiB of
-    ODS + EDS).  Returns one BlockResult per block."""
+    ODS + EDS); the blocks are staged in windows of at most `max_stage_bytes`
+    of txs (page-locked host memory).  Returns one BlockResult per block."""
     import torch
     ctx = ctx or default_context()
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    blocks = list(blocks)
+    out, w0, size = [], 0, 0
+    for i, txs in enumerate(blocks):
+        b = sum(map(len, txs)) + 32
+        if i > w0 and size + b > max_stage_bytes:
+            out += _replay_window(blocks[w0:i], max_square_size, subtree_root_threshold, ctx, dev, max_batch)
+            w0, size = i, 0
+        size += b
+    out += _replay_window(blocks[w0:], max_square_size, subtree_root_threshold, ctx, dev, max_batch)
+    if data_hashes is not None:
+        for r, h in zip(out, data_hashes):
+            r.accepted = r.error is None and r.data_root == bytes(h)
+    return out
+
+
+def _replay_window(blocks, max_square_size, subtree_root_threshold, ctx, dev, max_batch):
+    import torch
+    if not blocks:
+        return []
     stream = torch.cuda.current_stream(dev).cuda_stream
     pinned, host, lay = _stage_txs(blocks)
     out = []
@@ -164,7 +185,4 @@ def replay(blocks, data_hashes=None, max_square_size: int = SQUARE_SIZE_UPPER_BO
                 out[i].error = _push_order_message(d_ods[j].cpu().numpy(), k, ctx.push_order_detail_at(j))
         del d_ods, d_eds
     torch.cuda.current_stream(dev).synchronize()   # the pinned staging outlives every read of it
-    if data_hashes is not None:
-        for r, h in zip(out, data_hashes):
-            r.accepted = r.error is None and r.data_root == bytes(h)
     return out

@@ -99,3 +99,7 @@ def test_replay_many_same_size(ctx):
     # the same blocks in batches of at most 7 squares (4 batches, the last ragged)
     chunked = replay.replay(blocks, max_square_size=32, ctx=ctx, max_batch=7)
     assert [r.data_root for r in chunked] == [r.data_root for r in res]
+    # and staged in windows of about 3 blocks' txs
+    window = 3 * sum(map(len, blocks[0])) + 100
+    windowed = replay.replay(blocks, max_square_size=32, ctx=ctx, max_stage_bytes=window)
+    assert [r.data_root for r in windowed] == [r.data_root for r in res]
