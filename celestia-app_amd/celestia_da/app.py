@@ -1,0 +1,118 @@
+"""Mirror of the app-level DA entry points of celestia-app.
+
+References:
+  * app/extend_block.go:13-26 -- ExtendBlock(data, appVersion): square.Construct
+    with the version's SquareSizeUpperBound / SubtreeRootThreshold, then
+    da.ExtendShares(shares.ToBytes(square));
+  * app/extend_block.go:28-32 -- IsEmptyBlock: no txs;
+  * app/process_proposal.go:122-152 -- the data-availability half of
+    ProcessProposal: Construct (reject on error), the proposed square size
+    against the computed one, ExtendShares, NewDataAvailabilityHeader and the
+    DAH hash against the header's DataHash, each rejection logged with the
+    reason text reproduced here;
+  * pkg/appconsts/versioned_consts.go:20-27 -- both versioned constants are
+    v1's for every app version.
+
+Each block is one GPU submission (cda_construct_extend_dah: txs -> square ->
+EDS -> roots -> data root); for many blocks, celestia_da.replay batches the
+squares of one size.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib, da, rsmt2d, square, wrapper
+from ._lib import NMT_ROOT_SIZE, SHARE_SIZE, PushOrderError
+
+LATEST_VERSION = 2   # pkg/appconsts/versioned_consts.go:9 (v2.Version)
+
+
+def square_size_upper_bound(app_version: int = LATEST_VERSION) -> int:
+    """appconsts.SquareSizeUpperBound (versioned_consts.go:25-27): v1's for every version."""
+    return square.SQUARE_SIZE_UPPER_BOUND
+
+
+def subtree_root_threshold(app_version: int = LATEST_VERSION) -> int:
+    """appconsts.SubtreeRootThreshold (versioned_consts.go:20-22): v1's for every version."""
+    return square.SUBTREE_ROOT_THRESHOLD
+
+
+def is_empty_block(txs, app_version: int = LATEST_VERSION) -> bool:
+    """IsEmptyBlock (extend_block.go:30-32)."""
+    return len(txs) == 0
+
+
+def extend_block(txs, app_version: int = LATEST_VERSION, ctx=None) -> rsmt2d.ExtendedDataSquare:
+    """ExtendBlock (extend_block.go:15-26): the block's EDS, its row / column
+    roots and data root from ONE device submission; the roots seed the
+    constructor's trees as da.extend_shares does.  Raises SquareError with
+    go-square's message when Construct fails."""
+    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    codec = rsmt2d.LeoRSCodec(ctx) if ctx is not None else da.default_codec()
+    try:
+        k, eds, rows, cols, root, _ = square.construct_extend_dah(txs, ub, thr, want_eds=True, ctx=ctx)
+    except PushOrderError:   # Construct orders every namespace: not reachable from txs, kept for parity
+        sq = square.construct(txs, ub, thr, ctx=ctx)
+        return da.extend_shares(list(sq))
+    W = 2 * k
+    arr = np.frombuffer(bytearray(eds), dtype=np.uint8).reshape(W, W, SHARE_SIZE)
+    r = np.frombuffer(b"".join(rows), dtype=np.uint8).reshape(W, NMT_ROOT_SIZE).copy()
+    c = np.frombuffer(b"".join(cols), dtype=np.uint8).reshape(W, NMT_ROOT_SIZE).copy()
+    return rsmt2d.ExtendedDataSquare(arr, codec, wrapper.new_constructor(k), roots=(r, c, root))
+
+
+@dataclass
+class ProposalVerdict:
+    """ProcessProposal's DA decision for one block (:122-152)."""
+    accept: bool
+    reason: str | None = None     # the rejection log's reason (logInvalidPropBlock / ...Error)
+    square_size: int = 0
+    data_root: bytes | None = None
+
+
+def _reason_square(err) -> str:
+    return f"failure to compute data square from transactions: {err}"
+
+
+def process_proposal_da(txs, square_size: int, data_hash: bytes, app_version: int = LATEST_VERSION,
+                        ctx=None) -> ProposalVerdict:
+    """The data-availability checks of ProcessProposal (:122-152) for one
+    block: txs, the proposer's BlockData.SquareSize and Header.DataHash."""
+    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    try:
+        k, _, _, _, root, _ = square.construct_extend_dah(txs, ub, thr, ctx=ctx)
+    except _lib.SquareError as e:
+        return ProposalVerdict(False, _reason_square(e))
+    except PushOrderError as e:
+        return ProposalVerdict(False, f"failure to create new data availability header: {e}")
+    return _verdict(k, root, square_size, data_hash)
+
+
+def _verdict(k: int, root: bytes, square_size: int, data_hash: bytes) -> ProposalVerdict:
+    if k != square_size:
+        return ProposalVerdict(False, "proposed square size differs from calculated square size", k)
+    if root != bytes(data_hash):
+        return ProposalVerdict(False, f"proposed data root {bytes(data_hash).hex().upper()} differs from "
+                                      f"calculated data root {root.hex().upper()}", k, root)
+    return ProposalVerdict(True, None, k, root)
+
+
+def process_proposals_da(blocks, square_sizes, data_hashes, app_version: int = LATEST_VERSION, ctx=None,
+                         device=None) -> list[ProposalVerdict]:
+    """process_proposal_da over many blocks, the squares of one size extended
+    as one device batch (celestia_da.replay)."""
+    from . import replay
+    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    out = []
+    for r, ss, h in zip(replay.replay(blocks, None, ub, thr, ctx=ctx, device=device), square_sizes, data_hashes):
+        if r.error is not None:
+            if r.square_size == 0:
+                out.append(ProposalVerdict(False, _reason_square(r.error)))
+            else:
+                out.append(ProposalVerdict(False, f"failure to create new data availability header: {r.error}",
+                                           r.square_size))
+        else:
+            out.append(_verdict(r.square_size, r.data_root, ss, h))
+    return out

@@ -1,0 +1,88 @@
+"""App-level DA entry points (celestia_da.app): ExtendBlock / IsEmptyBlock
+(app/extend_block.go:13-32) and the DA checks of ProcessProposal
+(app/process_proposal.go:122-152) with the reference's rejection reasons.
+
+Pinned by mainnet block 408 (its header DataHash and square size, and the
+ODS decoded from the reference fixture x/blob/test/testdata/block_response.json).
+"""
+import numpy as np
+import pytest
+
+from celestia_da import app, blobfactory, da
+from celestia_da import square as gsq
+from test_square import block408, block408_ods
+
+
+def test_versioned_consts():
+    for v in (1, 2, app.LATEST_VERSION):
+        assert app.square_size_upper_bound(v) == 128
+        assert app.subtree_root_threshold(v) == 64
+
+
+def test_is_empty_block():
+    assert app.is_empty_block([])
+    assert not app.is_empty_block([b"x"])
+
+
+def _bad_block():
+    rng = np.random.default_rng(3)
+    return blobfactory.random_block(12, 1, 2) + [blobfactory.normal_tx(rng, 100)]
+
+
+@pytest.mark.gpu
+def test_extend_block_block408(ctx):
+    txs, k, data_hash = block408()
+    eds = app.extend_block(txs, ctx=ctx)
+    assert eds.width() == 2 * k
+    assert eds.array()[:k, :k].tobytes() == block408_ods()
+    dah = da.new_data_availability_header(eds)
+    assert dah.hash() == data_hash
+    # the same EDS and roots as Construct then ExtendShares as two calls
+    ref = da.extend_shares(list(gsq.construct(txs)))
+    assert np.array_equal(ref.array(), eds.array())
+    assert ref.row_roots() == eds.row_roots() and ref.col_roots() == eds.col_roots()
+
+
+@pytest.mark.gpu
+def test_extend_block_errors_and_empty(ctx):
+    from celestia_da import SquareError
+    with pytest.raises(SquareError, match="normal transaction at index 3"):
+        app.extend_block(_bad_block(), ctx=ctx)
+    eds = app.extend_block([], ctx=ctx)
+    assert eds.width() == 2
+    assert da.new_data_availability_header(eds).hash() == da.min_data_availability_header().hash()
+
+
+@pytest.mark.gpu
+def test_process_proposal_da_reasons(ctx):
+    txs, k, data_hash = block408()
+    v = app.process_proposal_da(txs, k, data_hash, ctx=ctx)
+    assert v.accept and v.reason is None and v.data_root == data_hash
+    v = app.process_proposal_da(txs, 2 * k, data_hash, ctx=ctx)
+    assert not v.accept and v.reason == "proposed square size differs from calculated square size"
+    wrong = bytes(32)
+    v = app.process_proposal_da(txs, k, wrong, ctx=ctx)
+    assert not v.accept
+    assert v.reason == (f"proposed data root {'00' * 32} differs from calculated data root "
+                        f"{data_hash.hex().upper()}")
+    v = app.process_proposal_da(_bad_block(), 8, wrong, ctx=ctx)
+    assert not v.accept and v.reason.startswith(
+        "failure to compute data square from transactions: normal transaction at index 3")
+
+
+@pytest.mark.gpu
+def test_process_proposals_da_batch_equals_per_block(ctx):
+    txs, k, data_hash = block408()
+    blocks = [txs, _bad_block(), blobfactory.full_block(5, 64), [], txs, blobfactory.full_block(6, 128)]
+    sizes, hashes = [], []
+    for i, b in enumerate(blocks):
+        try:
+            kk, _, _, _, root, _ = gsq.construct_extend_dah(b, ctx=ctx)
+        except Exception:
+            kk, root = 8, bytes(32)
+        sizes.append(kk + (i == 4))           # block 4: a wrong proposed size
+        hashes.append(root if i != 2 else bytes(32))   # block 2: a wrong data hash
+    got = app.process_proposals_da(blocks, sizes, hashes, ctx=ctx)
+    want = [app.process_proposal_da(b, s, h, ctx=ctx) for b, s, h in zip(blocks, sizes, hashes)]
+    assert got == want
+    assert [v.accept for v in got] == [True, False, False, True, False, True]
