@@ -10,6 +10,10 @@ References:
     against the computed one, ExtendShares, NewDataAvailabilityHeader and the
     DAH hash against the header's DataHash, each rejection logged with the
     reason text reproduced here;
+  * app/prepare_proposal.go:48-89 -- the data-availability half of
+    PrepareProposal: square.Build over the filtered txs, ExtendShares,
+    NewDataAvailabilityHeader; the block data carries the kept txs, the
+    square size and the data root;
   * pkg/appconsts/versioned_consts.go:20-27 -- both versioned constants are
     v1's for every app version.
 
@@ -61,6 +65,23 @@ def extend_block(txs, app_version: int = LATEST_VERSION, ctx=None) -> rsmt2d.Ext
     r = np.frombuffer(b"".join(rows), dtype=np.uint8).reshape(W, NMT_ROOT_SIZE).copy()
     c = np.frombuffer(b"".join(cols), dtype=np.uint8).reshape(W, NMT_ROOT_SIZE).copy()
     return rsmt2d.ExtendedDataSquare(arr, codec, wrapper.new_constructor(k), roots=(r, c, root))
+
+
+@dataclass
+class BlockData:
+    """core.Data as PrepareProposal returns it (prepare_proposal.go:84-88)."""
+    txs: list
+    square_size: int
+    hash: bytes
+
+
+def prepare_proposal_da(txs, app_version: int = LATEST_VERSION, ctx=None) -> BlockData:
+    """PrepareProposal's DA steps (:48-89) on already filtered txs: Build
+    (prioritised: normal txs, then blob txs, what fits), extend, DAH hash --
+    one device submission.  The reference panics where this raises."""
+    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    k, _, _, _, root, kept = square.construct_extend_dah(txs, ub, thr, build_mode=True, ctx=ctx)
+    return BlockData([txs[i] for i in kept], k, root)
 
 
 @dataclass

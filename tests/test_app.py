@@ -86,3 +86,22 @@ def test_process_proposals_da_batch_equals_per_block(ctx):
     want = [app.process_proposal_da(b, s, h, ctx=ctx) for b, s, h in zip(blocks, sizes, hashes)]
     assert got == want
     assert [v.accept for v in got] == [True, False, False, True, False, True]
+
+
+@pytest.mark.gpu
+def test_prepare_then_process(ctx):
+    """A proposal built by prepare_proposal_da is accepted by
+    process_proposal_da (the round trip every honest block takes); Build
+    drops what does not fit and reorders normal txs first."""
+    rng = np.random.default_rng(9)
+    txs = blobfactory.random_block(21, 3, 20, (1, 2), (1, 20000)) + [blobfactory.normal_tx(rng, 300)]
+    bd = app.prepare_proposal_da(txs, ctx=ctx)
+    assert bd.txs[0] is txs[0] and txs[-1] in bd.txs[:4]
+    sq, kept = gsq.build(txs, 128, 64, ctx=ctx)
+    assert bd.txs == kept and bd.square_size == sq.size()
+    v = app.process_proposal_da(bd.txs, bd.square_size, bd.hash, ctx=ctx)
+    assert v.accept, v.reason
+    big = blobfactory.random_block(11, 2, 400, (1, 2), (20000, 60000))
+    bd = app.prepare_proposal_da(big, ctx=ctx)
+    assert bd.square_size == 128 and 0 < len(bd.txs) < len(big)
+    assert app.process_proposal_da(bd.txs, 128, bd.hash, ctx=ctx).accept
