@@ -61,7 +61,7 @@ EXPORTED = (
     "cda_extend_dah_inplace_device", "cda_reserve",
     "cda_rs_encode", "cda_data_root", "cda_push_order_detail", "cda_push_order_detail_at", "cda_set_profiling", "cda_stage_times",
     "cda_split_rows", "cda_split_cols", "cda_split_combine",
-    "cda_square_layout", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
+    "cda_square_layout", "cda_square_tx_share_range", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
     "cda_blob_commitments", "cda_blob_commitments_device",
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
     "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
@@ -161,6 +161,8 @@ def load(path: str | None = None):
         u64p = C.POINTER(C.c_uint64)
         L.cda_square_layout.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, u32p, u32p,
                                         u32p, u32p, C.c_uint32, u32p]
+        L.cda_square_tx_share_range.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                                u32p, u32p, C.POINTER(C.c_int)]
         L.cda_square_construct.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, u8p,
                                            C.c_size_t, u32p, u32p, u32p]
         L.cda_construct_extend_dah.argtypes = [ctxp, u8p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, u8p,

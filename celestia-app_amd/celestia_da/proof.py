@@ -1,7 +1,8 @@
 """Mirror of pkg/proof (ShareProof, NewShareInclusionProofFromEDS) and
 pkg/inclusion GetCommitment over a device-resident square (libcda.so).
 
-Reference: pkg/proof/proof.go:77-206, pkg/proof/proof.pb.go (ShareProof,
+Reference: pkg/proof/proof.go:22-206 (NewTxInclusionProof,
+NewShareInclusionProof, NewShareInclusionProofFromEDS), pkg/proof/proof.pb.go (ShareProof,
 RowProof, NMTProof, Proof field names), pkg/inclusion/get_commit.go:12-30.
 The square is extended once (`ResidentSquare`); the EDS, every row-tree
 level and the data-root tree stay in HBM, so each proof is a gather.
@@ -139,3 +140,49 @@ class ResidentSquare:
         self.ctx.check(self.ctx.lib.cda_square_blob_commitments(self.h, s, ln, n, subtree_root_threshold, ptr(out)))
         b = out.tobytes()
         return [b[32 * i:32 * (i + 1)] for i in range(n)]
+
+
+TX_NAMESPACE = b"\x00" * 28 + b"\x01"            # go-square namespace.TxNamespace
+PAY_FOR_BLOB_NAMESPACE = b"\x00" * 28 + b"\x04"  # namespace.PayForBlobNamespace
+
+
+def tx_share_range(txs, tx_index: int, max_square_size: int = 128, subtree_root_threshold: int = 64):
+    """builder.FindTxShareRange of square.Construct's layout: (start, end,
+    namespace) -- the tx namespace for a normal tx, the PFB namespace for a
+    blob tx (proof.go:51-57 getTxNamespace).  Host only."""
+    from .square import _flatten, _u64p
+    L = _lib.load()
+    buf, off = _flatten(txs)
+    s, e, pfb = C.c_uint32(), C.c_uint32(), C.c_int()
+    rc = L.cda_square_tx_share_range(None, ptr(buf), _u64p(off), len(txs), max_square_size, subtree_root_threshold,
+                                     tx_index, C.byref(s), C.byref(e), C.byref(pfb))
+    if rc != _lib.CDA_OK:
+        msg = L.cda_last_error(None).decode()
+        raise (_lib.SquareError if rc == _lib.CDA_ERR_SQUARE else _lib.CdaError)(rc, msg)
+    return s.value, e.value, PAY_FOR_BLOB_NAMESPACE if pfb.value else TX_NAMESPACE
+
+
+def new_share_inclusion_proof(ods, namespace: bytes, start: int, end: int, ctx=None) -> ShareProof:
+    """NewShareInclusionProof (proof.go:59-73): extend the square, prove the
+    range.  ods: the square's shares (bytes, a list of shares or an array)."""
+    if isinstance(ods, (bytes, bytearray, memoryview)):
+        ods = np.frombuffer(ods, dtype=np.uint8)
+    elif isinstance(ods, list):
+        ods = np.frombuffer(b"".join(ods), dtype=np.uint8)
+    sq = ResidentSquare(ods, ctx)
+    try:
+        return sq.share_proof(namespace, start, end)
+    finally:
+        sq.close()
+
+
+def new_tx_inclusion_proof(txs, tx_index: int, app_version: int = 2, ctx=None) -> ShareProof:
+    """NewTxInclusionProof (proof.go:22-49): the share proof of the shares that
+    hold tx tx_index of the block, in the square square.Construct builds."""
+    from . import square
+    if tx_index >= len(txs):
+        raise _lib.CdaError(_lib.CDA_ERR_INVALID, f"txIndex {tx_index} out of bounds")
+    ub, thr = square.SQUARE_SIZE_UPPER_BOUND, square.SUBTREE_ROOT_THRESHOLD   # appconsts, every version
+    start, end, ns = tx_share_range(txs, tx_index, ub, thr)
+    sq = square.construct(txs, ub, thr, ctx=ctx)
+    return new_share_inclusion_proof(sq.to_bytes(), ns, start, end, ctx)

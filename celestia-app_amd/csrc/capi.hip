@@ -328,6 +328,45 @@ int cda_split_combine(cda_ctx* ctx, const void* d_row_subtree_slots, uint32_t pa
     });
 }
 
+int cda_square_tx_share_range(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs,
+                              uint32_t max_square_size, uint32_t threshold, uint32_t tx_index, uint32_t* start,
+                              uint32_t* end, int* is_pfb) {
+    // Host-only (no device work): usable without a context.
+    auto run = [&](std::string* err) -> int {
+        if (!start || !end || (n_txs && (!txs || !tx_off))) {
+            *err = "null buffer";
+            return CDA_ERR_INVALID;
+        }
+        cda::square::Plan p;
+        if (plan_square(txs, tx_off, n_txs, max_square_size, threshold, CDA_SQUARE_CONSTRUCT, &p, err))
+            return CDA_ERR_SQUARE;
+        if (tx_index >= p.unit_start.size()) {
+            char b[64];
+            snprintf(b, sizeof b, "txIndex %u out of range", tx_index);
+            *err = b;
+            return CDA_ERR_INVALID;
+        }
+        *start = p.unit_start[tx_index];
+        *end = p.unit_end[tx_index];
+        if (is_pfb) *is_pfb = tx_index >= p.n_normal;
+        return CDA_OK;
+    };
+    if (!ctx) {
+        tl_err.msg.clear();
+        try {
+            return run(&tl_err.msg);
+        } catch (const std::bad_alloc&) {
+            tl_err.msg = "host allocation failed";
+            return CDA_ERR_OOM;
+        }
+    }
+    return guarded(ctx, [&](cda::Engine& e) -> int {
+        std::string err;
+        const int rc = run(&err);
+        return rc ? e.fail(rc, err) : CDA_OK;
+    });
+}
+
 int cda_square_layout(cda_ctx* ctx, const uint8_t* txs, const uint64_t* tx_off, uint32_t n_txs,
                       uint32_t max_square_size, uint32_t threshold, int mode, uint32_t* square_size, uint32_t* kept,
                       uint32_t* n_kept, uint32_t* share_indexes, uint32_t share_index_cap, uint32_t* n_share_indexes) {

@@ -18,6 +18,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <string_view>
+#include <unordered_map>
 
 namespace cda {
 namespace square {
@@ -264,7 +266,11 @@ struct CompactCounter {   // shares.CompactShareCounter
 };
 
 // CompactShareSplitter: units are varint-delimited; appends whole shares.
-void compact_shares(const uint8_t* ns, const std::vector<Span>& units, std::vector<uint8_t>& out, uint32_t* n_out) {
+// ranges (optional): per unit, WriteTx's recorded range -- from the share the
+// unit starts in (the number of completed shares before it) to Count() after
+// it (completed shares, plus the pending one if it holds data).
+void compact_shares(const uint8_t* ns, const std::vector<Span>& units, std::vector<uint8_t>& out, uint32_t* n_out,
+                    std::vector<uint32_t>* r_start = nullptr, std::vector<uint32_t>* r_end = nullptr) {
     *n_out = 0;
     if (units.empty()) return;
     const size_t base = out.size();
@@ -300,6 +306,7 @@ void compact_shares(const uint8_t* ns, const std::vector<Span>& units, std::vect
             cur[res_at + 3] = (uint8_t)at;
             reserved_set = true;
         }
+        if (r_start) r_start->push_back(*n_out);
         size_t off = 0;
         while (off < unit.size()) {
             const size_t room = kShare - cur.size();
@@ -311,6 +318,7 @@ void compact_shares(const uint8_t* ns, const std::vector<Span>& units, std::vect
                 start_share(false);
             }
         }
+        if (r_end) r_end->push_back(*n_out + (cur.size() > res_at + 4 ? 1u : 0u));
     }
     if (cur.size() > res_at + 4) flush();
     uint8_t* first = out.data() + base;
@@ -467,7 +475,8 @@ int plan(const uint8_t* txs, const uint64_t* off, uint32_t n, uint32_t max_ss, u
     std::stable_sort(elems.begin(), elems.end(),
                      [](const Element& a, const Element& b) { return ns_compare(a, b) < 0; });
     uint32_t n_tx_shares = 0, n_pfb_shares = 0;
-    compact_shares(kTxNs, normal, P.compact, &n_tx_shares);
+    std::vector<uint32_t> tx_s, tx_e, pfb_s, pfb_e;
+    compact_shares(kTxNs, normal, P.compact, &n_tx_shares, &tx_s, &tx_e);
 
     std::vector<std::vector<uint32_t>> pfb_idx(pfb_inner.size());
     for (size_t i = 0; i < pfb_inner.size(); i++) pfb_idx[i].assign(pfb_nblobs[i], 0);
@@ -534,7 +543,23 @@ int plan(const uint8_t* txs, const uint64_t* off, uint32_t n, uint32_t max_ss, u
             P.share_index_pfb.push_back((uint32_t)i);
         }
     }
-    compact_shares(kPfbNs, pfb_units, P.compact, &n_pfb_shares);
+    compact_shares(kPfbNs, pfb_units, P.compact, &n_pfb_shares, &pfb_s, &pfb_e);
+    // FindTxShareRange: the tx writer's ranges, then the PFB writer's offset by
+    // the tx writer's share count; a repeated unit reports its last copy's range
+    auto ranges = [&](const std::vector<Span>& units, const std::vector<uint32_t>& s0, const std::vector<uint32_t>& e0,
+                      uint32_t base) {
+        std::unordered_map<std::string_view, size_t> last;
+        for (size_t i = 0; i < units.size(); i++)
+            last[std::string_view(reinterpret_cast<const char*>(units[i].p), units[i].n)] = i;
+        for (size_t i = 0; i < units.size(); i++) {
+            const size_t j = last[std::string_view(reinterpret_cast<const char*>(units[i].p), units[i].n)];
+            P.unit_start.push_back(base + s0[j]);
+            P.unit_end.push_back(base + e0[j]);
+        }
+    };
+    ranges(normal, tx_s, tx_e, 0);
+    ranges(pfb_units, pfb_s, pfb_e, n_tx_shares);
+    P.n_normal = (uint32_t)normal.size();
     if (pfb_counter.size() < (int64_t)n_pfb_shares) {
         *err = fmt("pfbCounter.Size() < pfbTxWriter.Count(): %lld < %lld", pfb_counter.size(), n_pfb_shares);
         return -1;

@@ -55,6 +55,12 @@ struct Plan {
     std::vector<uint32_t> share_indexes;   // per PFB (square order) per blob: start share (IndexWrapper.share_indexes)
     std::vector<uint32_t> share_index_pfb; // PFB ordinal of each entry of share_indexes
     uint32_t n_blobs = 0;
+    // builder.FindTxShareRange per kept tx (normal txs, then PFBs): shares
+    // [unit_start, unit_end) of the square; equal units (same bytes, same
+    // writer) all report the last one's range, as the go-square splitters key
+    // their range maps by the tx hash (shares.CompactShareSplitter.ShareRanges)
+    std::vector<uint32_t> unit_start, unit_end;
+    uint32_t n_normal = 0;             // kept normal txs (units [0, n_normal) are in the tx namespace)
 };
 
 enum Mode { kConstruct = 0, kBuild = 1 };

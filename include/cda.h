@@ -335,6 +335,16 @@ int cda_square_layout(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, 
                       uint32_t max_square_size, uint32_t threshold, int mode, uint32_t *square_size, uint32_t *kept,
                       uint32_t *n_kept, uint32_t *share_indexes, uint32_t share_index_cap, uint32_t *n_share_indexes);
 
+/* go-square builder.FindTxShareRange for the square.Construct layout of txs
+ * (pkg/proof/proof.go:22-49 NewTxInclusionProof): the shares [start, end) of
+ * the square holding kept tx tx_index (normal txs, then blob txs as their
+ * IndexWrapper in the PFB namespace; *is_pfb says which).  Equal txs report
+ * the last copy's range (the splitters key ranges by tx hash).  Host only;
+ * ctx may be NULL.  CDA_ERR_INVALID "txIndex %u out of range". */
+int cda_square_tx_share_range(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, uint32_t n_txs,
+                              uint32_t max_square_size, uint32_t threshold, uint32_t tx_index, uint32_t *start,
+                              uint32_t *end, int *is_pfb);
+
 /* The square's k*k shares (row-major) into ods (host, ods_capacity bytes;
  * max_square_size^2 * 512 always suffices).  Shares are written on the GPU. */
 int cda_square_construct(cda_ctx *ctx, const uint8_t *txs, const uint64_t *tx_off, uint32_t n_txs,

@@ -161,6 +161,57 @@ def compact_shares(ns: bytes, units) -> list:
     return [bytes(s) for s in shares]
 
 
+def compact_share_ranges(units) -> list:
+    """CompactShareSplitter.WriteTx's recorded share range per unit, as
+    (start, end): start = the shares completed before the unit is written,
+    end = Count() after it (completed shares + the pending one if it holds
+    data).  The splitter keys its range map by the tx hash, so equal units
+    all report the range of the last one written (ShareRanges)."""
+    out, done, fill = [], 0, None      # fill: bytes in the pending share (None: no share yet)
+    for u in units:
+        n = len(_enc_varint(len(u))) + len(u)
+        if fill is None:
+            fill = NS_SIZE + 1 + 4 + 4          # first share: ns, info, sequence length, reserved
+        start = done
+        while n:
+            take = min(SHARE_SIZE - fill, n)
+            fill += take
+            n -= take
+            if fill == SHARE_SIZE:
+                done += 1
+                fill = NS_SIZE + 1 + 4          # continuation: ns, info, reserved
+        header = NS_SIZE + 1 + 4 + (4 if done == 0 else 0)
+        out.append((start, done + (1 if fill > header else 0)))
+    last = {bytes(u): i for i, u in enumerate(units)}
+    return [out[last[bytes(u)]] for u in units]
+
+
+def find_tx_share_range(txs, tx_index: int, max_square_size: int = 128,
+                        threshold: int = SUBTREE_ROOT_THRESHOLD):
+    """go-square builder.FindTxShareRange after square.Construct's layout
+    (pkg/proof/proof.go:22-49): (start, end, is_pfb) of kept tx tx_index --
+    normal txs in the tx namespace's compact shares, then blob txs as their
+    IndexWrapper in the PFB namespace's, offset by the tx shares."""
+    _, _, kept, share_idx = builder(txs, max_square_size, threshold, "construct")
+    normal, pfbs, at = [], [], 0
+    for t in kept:
+        bt = unmarshal_blob_tx(txs[t])
+        if bt is None:
+            normal.append(txs[t])
+        else:
+            inner, bl = bt
+            pfbs.append(marshal_index_wrapper(inner, share_idx[at:at + len(bl)]))
+            at += len(bl)
+    if tx_index >= len(normal) + len(pfbs):
+        raise ValueError(f"txIndex {tx_index} out of range")
+    if tx_index < len(normal):
+        s, e = compact_share_ranges(normal)[tx_index]
+        return s, e, False
+    n_tx = len(compact_shares(TX_NS, normal))
+    s, e = compact_share_ranges(pfbs)[tx_index - len(normal)]
+    return n_tx + s, n_tx + e, True
+
+
 def sparse_shares(ns: bytes, data: bytes, version: int = 0) -> list:
     out = []
     first = bytearray(ns + bytes([_info_byte(version, True)]) + len(data).to_bytes(4, "big"))

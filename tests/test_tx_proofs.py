@@ -1,0 +1,142 @@
+"""Transaction inclusion proofs: proof.NewTxInclusionProof (pkg/proof/proof.go:22-57)
+over go-square's builder.FindTxShareRange.
+
+CPU: cda_square_tx_share_range (csrc/square_plan.cpp, the compact-share
+splitters' recorded ranges) against the oracle's restatement
+(oracle/square.py find_tx_share_range) on every tx of several blocks --
+mainnet block 408, the reference test's shape (50 normal txs of 500 B, then
+50 blob txs with one 500-B blob: pkg/proof/proof_test.go:27-96), repeated
+txs (the splitters key ranges by tx hash) and txs that end exactly on a
+share boundary -- and the reference's error cases.
+GPU: the proofs of the indexes the reference test proves (first / last
+normal, first / last blob tx) and of every tx of block 408 verify against the
+oracle's row roots and data root (block 408: its header DataHash), and cover
+exactly the shares of the tx's compact range.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import proofs as opr
+import pyref
+import square as osq
+from celestia_da import CdaError, SquareError, _lib, blobfactory
+from celestia_da import proof as gpr
+from celestia_da import square as gsq
+from test_proofs import oracle_eds
+from test_square import block408
+
+
+def _reference_shape_block(seed=3):
+    rng = np.random.default_rng(seed)
+    normal = [blobfactory.normal_tx(rng, 500) for _ in range(50)]
+    blob_txs = blobfactory.random_block(seed, 0, 50, (1, 1), (500, 500))
+    return normal + blob_txs
+
+
+def _blocks():
+    rng = np.random.default_rng(11)
+    dup = [blobfactory.normal_tx(rng, 300) for _ in range(3)]
+    return {
+        "block408": block408()[0],
+        "reference_shape": _reference_shape_block(),
+        "normal_only": blobfactory.random_block(5, 30, 0),
+        "repeated": [dup[0], dup[1], dup[0], dup[2], dup[0]],
+        # 472 + 2 varint bytes fill the first share's 474, 476 + 2 a continuation's 478
+        "share_boundaries": [bytes([7]) * 472, bytes([8]) * 476, bytes([9]) * 10, bytes([1]) * 1000],
+        "many_blobs": blobfactory.random_block(8, 4, 40, (1, 3), (1, 9000), 3),
+    }
+
+
+def _c_range(txs, i):
+    buf, off = gsq._flatten(txs)
+    s, e, p = C.c_uint32(), C.c_uint32(), C.c_int()
+    L = _lib.load()
+    rc = L.cda_square_tx_share_range(None, gsq.ptr(buf), gsq._u64p(off), len(txs), 128, 64, i, C.byref(s), C.byref(e),
+                                     C.byref(p))
+    if rc != _lib.CDA_OK:
+        return "error", L.cda_last_error(None).decode()
+    return s.value, e.value, bool(p.value)
+
+
+@pytest.mark.parametrize("name", list(_blocks()))
+def test_tx_share_range_matches_oracle(name):
+    txs = _blocks()[name]
+    for i in range(len(txs) + 1):
+        try:
+            want = osq.find_tx_share_range(txs, i)
+        except ValueError as e:
+            want = ("error", str(e))
+        assert _c_range(txs, i) == want, (name, i)
+
+
+def test_tx_share_range_semantics():
+    b = _blocks()
+    # repeated txs report the last copy's range
+    r = [_c_range(b["repeated"], i) for i in range(5)]
+    assert r[0] == r[2] == r[4] and r[0] != r[1]
+    # exact fills: each tx owns one share
+    assert [_c_range(b["share_boundaries"], i)[:2] for i in range(3)] == [(0, 1), (1, 2), (2, 3)]
+    # the reference shape: normal txs in the tx namespace, blob txs in the PFB namespace after them
+    txs = b["reference_shape"]
+    s49, e49, ns49 = gpr.tx_share_range(txs, 49)
+    s50, e50, ns50 = gpr.tx_share_range(txs, 50)
+    assert ns49 == gpr.TX_NAMESPACE and ns50 == gpr.PAY_FOR_BLOB_NAMESPACE
+    assert e49 <= s50 + 1 and s50 >= 1
+
+
+def test_tx_inclusion_proof_errors():
+    with pytest.raises(CdaError, match="txIndex 0 out of bounds"):
+        gpr.new_tx_inclusion_proof([], 0)
+    txs = _reference_shape_block()
+    with pytest.raises(CdaError, match="txIndex 100 out of bounds"):
+        gpr.new_tx_inclusion_proof(txs, 100)
+    rng = np.random.default_rng(3)
+    bad = blobfactory.random_block(12, 1, 2) + [blobfactory.normal_tx(rng, 100)]
+    with pytest.raises(SquareError, match="normal transaction at index 3"):
+        gpr.tx_share_range(bad, 0)
+
+
+def _verify(txs, idx, data_hash=None):
+    """NewTxInclusionProof for each index, checked against the oracle."""
+    shares, k, _, _ = osq.builder(txs, 128, 64, "construct")
+    ods = np.frombuffer(b"".join(shares), dtype=np.uint8).reshape(-1, 512).copy()
+    eds, rows, cols, root = oracle_eds(ods, k)
+    if data_hash is not None:
+        assert root == data_hash
+    items = rows + cols
+    for i in idx:
+        s, e, pfb = osq.find_tx_share_range(txs, i)
+        ns = osq.PFB_NS if pfb else osq.TX_NS
+        p = gpr.new_tx_inclusion_proof(txs, i)
+        assert bytes([p.namespace_version]) + p.namespace_id == ns
+        assert p.data == [shares[j] for j in range(s, e)]
+        assert all(d[:29] == ns for d in p.data)
+        r0, r1 = s // k, (e - 1) // k
+        assert (p.row_proof.start_row, p.row_proof.end_row) == (r0, r1)
+        for q, r in enumerate(range(r0, r1 + 1)):
+            sp = p.share_proofs[q]
+            leaves = pyref.erasured_leaves([bytes(c) for c in eds[r]], k, r)
+            assert opr.nmt_verify_range(rows[r], sp.nodes, sp.start, sp.end, 2 * k, leaves[sp.start:sp.end])
+            rp = p.row_proof.proofs[q]
+            assert opr.rfc_verify(root, rp.total, rp.index, rp.leaf_hash, rp.aunts)
+            assert p.row_proof.row_roots[q] == items[r]
+
+
+@pytest.mark.gpu
+def test_tx_inclusion_proofs_reference_shape(ctx):
+    _verify(_reference_shape_block(), [0, 49, 50, 99])
+
+
+@pytest.mark.gpu
+def test_tx_inclusion_proofs_block408(ctx):
+    txs, _, data_hash = block408()
+    _verify(txs, range(len(txs)), data_hash)
+
+
+@pytest.mark.gpu
+def test_tx_inclusion_proofs_boundaries_and_repeats(ctx):
+    b = _blocks()
+    _verify(b["share_boundaries"], range(4))
+    _verify(b["repeated"], range(5))
