@@ -11,7 +11,11 @@ Restates, from their published algorithms (EXT modules, go.mod:9-13):
     aunts bottom-up);
   * pkg/inclusion/paths.go calculateCommitmentPaths +
     get_commit.go GetCommitment (subtree roots of the ODS half of each row).
-Used by tests/test_proofs.py against the GPU proofs.
+  * pkg/proof/share_proof.go:16-78 ShareProof.Validate / VerifyProof and
+    row_proof.go:13-51 RowProof.Validate, over nmt's VerifyInclusion with the
+    namespace size taken from the proof (the reference's fixture uses 33-byte
+    namespaces), pinned by that fixture (tests/golden/share_proof_valid.json).
+Used by tests/test_proofs.py and tests/test_tx_proofs.py against the GPU proofs.
 """
 from __future__ import annotations
 
@@ -96,6 +100,107 @@ def rfc_verify(root: bytes, total: int, index: int, leaf_hash: bytes, aunts) -> 
         right = compute(idx - k, tot - k, leaf, aunts[:-1])
         return None if right is None else pyref.sha256(b"\x01" + aunts[-1] + right)
     return compute(index, total, leaf_hash, list(aunts)) == root
+
+
+# ------------------------------------------------- ShareProof.Validate (generic ns)
+def _nmt_leaf(nsz: int, ndata: bytes) -> bytes:
+    ns = ndata[:nsz]
+    return ns + ns + pyref.sha256(b"\x00" + ndata)
+
+
+def _nmt_node(nsz: int, left: bytes, right: bytes) -> bytes:
+    lmin, lmax = left[:nsz], left[nsz:2 * nsz]
+    rmin, rmax = right[:nsz], right[nsz:2 * nsz]
+    mx = lmax if rmin == b"\xff" * nsz else rmax      # IgnoreMaxNamespace(true)
+    return lmin + mx + pyref.sha256(b"\x01" + left + right)
+
+
+def _nmt_split(n: int) -> int:
+    """nmt getSplitPoint: the largest power of two below n (0 for n = 1)."""
+    k = 1 << (n.bit_length() - 1)
+    return k >> 1 if k == n else k
+
+
+def nmt_verify_inclusion(root: bytes, nodes, start: int, end: int, nid: bytes, leaves) -> bool:
+    """nmt Proof.VerifyInclusion (ignore-max-namespace proofs): leaf hashes of
+    nid || leaf, the subtree that holds the range (size 2 * getSplitPoint(end))
+    from them and the proof nodes met on the way, then the remaining nodes
+    folded in on the right."""
+    nsz = len(nid)
+    hashes = [_nmt_leaf(nsz, nid + bytes(x)) for x in leaves]
+    rest = list(nodes)
+
+    def pop(a):
+        return a.pop(0) if a else None
+
+    def compute(lo, hi):
+        if hi - lo == 1:
+            return pop(hashes) if start <= lo < end else pop(rest)
+        if hi <= start or lo >= end:
+            return pop(rest)
+        k = _nmt_split(hi - lo)
+        left, right = compute(lo, lo + k), compute(lo + k, hi)
+        return left if right is None else _nmt_node(nsz, left, right)
+
+    h = compute(0, max(1, 2 * _nmt_split(end)))
+    while rest:
+        h = _nmt_node(nsz, h, rest.pop(0))
+    return h == root
+
+
+def merkle_proof_verify(root: bytes, total: int, index: int, leaf_hash: bytes, aunts, leaf: bytes) -> bool:
+    """go-square/merkle Proof.Verify: the leaf hash must be the leaf's, then the trail."""
+    if total < 0 or index < 0 or pyref.sha256(b"\x00" + leaf) != leaf_hash:
+        return False
+    return rfc_verify(root, total, index, leaf_hash, aunts)
+
+
+def row_proof_validate(rp: dict, root: bytes):
+    """RowProof.Validate(root) (row_proof.go:13-27): None or the error text."""
+    rows = rp["end_row"] - rp["start_row"] + 1
+    if rows != len(rp["row_roots"]):
+        return f"the number of rows {rows} must equal the number of row roots {len(rp['row_roots'])}"
+    if len(rp["proofs"]) != len(rp["row_roots"]):
+        return f"the number of proofs {len(rp['proofs'])} must equal the number of row roots {len(rp['row_roots'])}"
+    for p, r in zip(rp["proofs"], rp["row_roots"]):
+        if not merkle_proof_verify(root, p["total"], p["index"], p["leaf_hash"], p["aunts"], r):
+            return "row proof failed to verify"
+    return None
+
+
+def share_proof_validate(sp: dict, root: bytes):
+    """ShareProof.Validate(root): None when valid, else the reference's error
+    text.  sp: {data, share_proofs [{start, end, nodes}], namespace_id,
+    namespace_version, row_proof {row_roots, proofs [{total, index,
+    leaf_hash, aunts}], start_row, end_row}} with bytes values."""
+    if not sp.get("data"):
+        return "empty share proof"
+    n_in_proofs = sum(p["end"] - p["start"] for p in sp["share_proofs"])
+    rp = sp["row_proof"]
+    if len(sp["share_proofs"]) != len(rp["row_roots"]):
+        return (f"the number of share proofs {len(sp['share_proofs'])} must equal the number of row roots "
+                f"{len(rp['row_roots'])}")
+    if len(sp["data"]) != n_in_proofs:
+        return f"the number of shares {len(sp['data'])} must equal the number of shares in share proofs {n_in_proofs}"
+    for p in sp["share_proofs"]:
+        if p["start"] < 0:
+            return "proof index cannot be negative"
+        if p["end"] - p["start"] <= 0:
+            return "proof total must be positive"
+    err = row_proof_validate(rp, root)
+    if err is not None:
+        return err
+    # VerifyProof
+    if sp["namespace_version"] > 255:
+        return "share proof failed to verify"
+    nid = bytes([sp["namespace_version"]]) + sp["namespace_id"]
+    cursor = 0
+    for p, r in zip(sp["share_proofs"], rp["row_roots"]):
+        used = p["end"] - p["start"]
+        if not nmt_verify_inclusion(r, p["nodes"], p["start"], p["end"], nid, sp["data"][cursor:cursor + used]):
+            return "share proof failed to verify"
+        cursor += used
+    return None
 
 
 # ------------------------------------------------------------ GetCommitment

@@ -22,6 +22,7 @@ import pyref
 import square as osq
 from celestia_da import CdaError, blobfactory
 from celestia_da import proof as gpr
+from test_share_proof_validate import to_dict
 
 
 def constructed_square(seed, max_ss=32, n_blob_txs=12, blob_size=(1, 6000)):
@@ -90,6 +91,8 @@ def test_share_proofs_gpu(ctx, seed, max_ss):
         items = rows + cols
         for s, e in ranges(k, blobs):
             p = sq.share_proof(bytes(eds[s // k][s % k][:29]), s, e)
+            if len({bytes(eds[i // k][i % k][:29]) for i in range(s, e)}) == 1:   # one namespace: Validate applies
+                assert opr.share_proof_validate(to_dict(p), root) is None
             r0, r1 = s // k, (e - 1) // k
             assert (p.row_proof.start_row, p.row_proof.end_row) == (r0, r1)
             assert b"".join(p.data) == eds.reshape(-1, 512)[0:0].tobytes() + b"".join(

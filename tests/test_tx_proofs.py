@@ -25,6 +25,7 @@ from celestia_da import CdaError, SquareError, _lib, blobfactory
 from celestia_da import proof as gpr
 from celestia_da import square as gsq
 from test_proofs import oracle_eds
+from test_share_proof_validate import to_dict
 from test_square import block408
 
 
@@ -110,6 +111,7 @@ def _verify(txs, idx, data_hash=None):
         s, e, pfb = osq.find_tx_share_range(txs, i)
         ns = osq.PFB_NS if pfb else osq.TX_NS
         p = gpr.new_tx_inclusion_proof(txs, i)
+        assert opr.share_proof_validate(to_dict(p), root) is None
         assert bytes([p.namespace_version]) + p.namespace_id == ns
         assert p.data == [shares[j] for j in range(s, e)]
         assert all(d[:29] == ns for d in p.data)
