@@ -57,6 +57,23 @@ def case_txs(c):
 
 
 # ------------------------------------------------------------------ CPU tests
+def test_block408_blob_tx_decode():
+    """x/blob/test/decode_blob_tx_test.go:29-58: the block's last tx (index
+    273) is a BlobTx whose inner tx hashes to C55BDD3D...5D21 and whose blob
+    namespace is 0x00..08e5f679bf7116cb -- the decoded fixture and the
+    BlobTx parser both agree with the reference's assertions."""
+    import hashlib
+    txs, _, _ = block408()
+    assert len(txs) == 274
+    inner, blobs = osq.unmarshal_blob_tx(txs[273])
+    assert hashlib.sha256(inner).hexdigest().upper() == \
+        "C55BDD3DF3348A9F8D9206528051804754F009A1B9D0F69CCC2F9D4334215D21"
+    ns = bytes([blobs[0]["namespace_version"]]) + blobs[0]["namespace_id"]
+    assert ns == bytes(21) + bytes.fromhex("08e5f679bf7116cb")
+    # the C planner takes it as the block's one blob tx too: its index is kept last
+    assert gsq.layout(txs)[1][-1] == 273
+
+
 def test_block408_layout():
     txs, k, _ = block408()
     ss, kept, idx = gsq.layout(txs)
