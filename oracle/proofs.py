@@ -229,23 +229,55 @@ def subtree_root_coords(max_depth: int, min_depth: int, start: int, end: int):
             node = (node[0] - 1, node[1] // 2)
 
 
-def get_commitment(eds, k: int, start: int, share_len: int, threshold: int = 64) -> bytes:
-    """inclusion.GetCommitment from the EDS rows (subtree roots recomputed)."""
+WALK_LEFT, WALK_RIGHT = False, True      # pkg/inclusion/nmt_caching.go WalkInstruction
+
+
+def subtree_root_path(depth: int, pos: int):
+    """pkg/inclusion/paths.go genSubTreeRootPath: the walk from a tree's root
+    to node (depth, pos), most significant position bit first."""
+    return [bool(pos & (1 << i)) for i in range(depth - 1, -1, -1)]
+
+
+def commitment_paths(k: int, start: int, share_len: int, threshold: int = 64):
+    """pkg/inclusion/paths.go calculateCommitmentPaths: (row, walk) of every
+    subtree root a blob's commitment uses, walks relative to the ODS half of
+    the row tree."""
     import square
-    if start + share_len > k * k:
-        raise ValueError("cannot get commitment for blob that doesn't fit in square")
-    w = square.subtree_width(share_len, threshold)
-    start = -(-start // w) * w
+    start = square.next_share_index(start, share_len, threshold)
     start_row, end_row = start // k, (start + share_len - 1) // k
     nsi, nei = start % k, start + share_len - end_row * k
     max_depth = k.bit_length() - 1
-    min_depth = max_depth - (w.bit_length() - 1)
-    roots = []
+    min_depth = max_depth - (square.subtree_width(share_len, threshold).bit_length() - 1)
+    paths = []
     for r in range(start_row, end_row + 1):
         s0 = nsi if r == start_row else 0
         e0 = nei if r == end_row else k
-        leaves = pyref.erasured_leaves([bytes(c) for c in eds[r]], k, r)
         for depth, pos in subtree_root_coords(max_depth, min_depth, s0, e0):
-            size = 1 << (max_depth - depth)
-            roots.append(pyref.nmt_root_from_nodes(leaves[pos * size:(pos + 1) * size]))
+            paths.append((r, subtree_root_path(depth, pos)))
+    return paths
+
+
+def walk_subtree_root(leaf_nodes, walk):
+    """EDSSubTreeRootCacher.walk (pkg/inclusion/nmt_caching.go:40-78) on a
+    row tree given by its leaf nodes: the node reached from the root by the
+    walk; a walk deeper than the tree fails like the cache miss does."""
+    lo, hi = 0, len(leaf_nodes)
+    for step in walk:
+        if hi - lo < 2:
+            raise KeyError("did not find sub tree root")
+        mid = lo + split_point(hi - lo)
+        lo, hi = (mid, hi) if step else (lo, mid)
+    return pyref.nmt_root_from_nodes(leaf_nodes[lo:hi])
+
+
+def get_commitment(eds, k: int, start: int, share_len: int, threshold: int = 64) -> bytes:
+    """inclusion.GetCommitment (pkg/inclusion/get_commit.go:12-30) from the EDS
+    rows: each path is prefixed with WalkLeft (the ODS half of the 2k-leaf row
+    tree) and walked down that row's tree."""
+    if start + share_len > k * k:
+        raise ValueError("cannot get commitment for blob that doesn't fit in square")
+    roots = []
+    for r, walk in commitment_paths(k, start, share_len, threshold):
+        leaves = pyref.erasured_leaves([bytes(c) for c in eds[r]], k, r)
+        roots.append(walk_subtree_root(leaves, [WALK_LEFT] + walk))
     return pyref.merkle_root(roots)
