@@ -142,3 +142,36 @@ def test_tx_inclusion_proofs_boundaries_and_repeats(ctx):
     b = _blocks()
     _verify(b["share_boundaries"], range(4))
     _verify(b["repeated"], range(5))
+
+
+def _all_shares_block(seed=17):
+    """TestAllSharesInclusionProof's block (pkg/proof/proof_test.go:241-268):
+    testfactory.GenerateRandomTxs(243, 500) -- 243 normal txs of 500 B."""
+    rng = np.random.default_rng(seed)
+    return [blobfactory.normal_tx(rng, 500) for _ in range(243)]
+
+
+def test_all_shares_block_layout():
+    """The reference asserts the square holds 256 shares, all in the tx
+    namespace (ParseNamespace over [0, 256))."""
+    shares, k, _, _ = osq.builder(_all_shares_block(), 128, 64, "construct")
+    assert (len(shares), k) == (256, 16)
+    assert all(s[:29] == osq.TX_NS for s in shares)
+    s, e, pfb = osq.find_tx_share_range(_all_shares_block(), 242)
+    assert (e, pfb) == (256, False)
+
+
+@pytest.mark.gpu
+def test_all_shares_inclusion_proof(ctx):
+    """NewShareInclusionProof(square, TxNamespace, [0, 256)) validates against
+    the data root (proof_test.go:241-268)."""
+    shares, k, _, _ = osq.builder(_all_shares_block(), 128, 64, "construct")
+    ods = np.frombuffer(b"".join(shares), dtype=np.uint8).reshape(-1, 512).copy()
+    _, rows, _, root = oracle_eds(ods, k)
+    p = gpr.new_share_inclusion_proof(ods, osq.TX_NS, 0, 256)
+    assert opr.share_proof_validate(to_dict(p), root) is None
+    assert (p.row_proof.start_row, p.row_proof.end_row) == (0, k - 1)
+    assert p.data == shares and p.row_proof.row_roots == rows[:k]
+    bad = to_dict(p)
+    bad["data"] = [bytes(512)] + bad["data"][1:]
+    assert opr.share_proof_validate(bad, root) is not None
