@@ -107,13 +107,20 @@ def process_proposal_da(txs, square_size: int, data_hash: bytes, app_version: in
     except _lib.SquareError as e:
         return ProposalVerdict(False, _reason_square(e))
     except PushOrderError as e:
-        return ProposalVerdict(False, f"failure to create new data availability header: {e}")
+        # the reference checks the proposed size before it extends (:133-136)
+        k = square.layout(txs, ub, thr)[0]
+        if k != square_size:
+            return ProposalVerdict(False, _REASON_SIZE, k)
+        return ProposalVerdict(False, f"failure to create new data availability header: {e}", k)
     return _verdict(k, root, square_size, data_hash)
+
+
+_REASON_SIZE = "proposed square size differs from calculated square size"
 
 
 def _verdict(k: int, root: bytes, square_size: int, data_hash: bytes) -> ProposalVerdict:
     if k != square_size:
-        return ProposalVerdict(False, "proposed square size differs from calculated square size", k)
+        return ProposalVerdict(False, _REASON_SIZE, k)
     if root != bytes(data_hash):
         return ProposalVerdict(False, f"proposed data root {bytes(data_hash).hex().upper()} differs from "
                                       f"calculated data root {root.hex().upper()}", k, root)
@@ -131,6 +138,8 @@ def process_proposals_da(blocks, square_sizes, data_hashes, app_version: int = L
         if r.error is not None:
             if r.square_size == 0:
                 out.append(ProposalVerdict(False, _reason_square(r.error)))
+            elif r.square_size != ss:   # size before the extend step's error (:133-136)
+                out.append(ProposalVerdict(False, _REASON_SIZE, r.square_size))
             else:
                 out.append(ProposalVerdict(False, f"failure to create new data availability header: {r.error}",
                                            r.square_size))
