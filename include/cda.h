@@ -120,7 +120,11 @@ int cda_dah_from_eds(cda_ctx *ctx, const uint8_t *eds, uint32_t w, uint8_t *row_
 
 /* ExtendShares + NewDataAvailabilityHeader in one device submission. eds may be
  * NULL when the caller only needs the roots. On CDA_ERR_PUSH_ORDER the EDS is
- * still written (ExtendShares succeeds; the error belongs to the DAH step). */
+ * still written (ExtendShares succeeds; the error belongs to the DAH step), and
+ * so are the roots and data root: those of the reference's fraud tooling,
+ * NewDataAvailabilityHeader over test/util/malicious/tree.go's BlindTrees (no
+ * order check; the hashing never depends on it).  The same holds per square in
+ * the batch entry points. */
 int cda_extend_dah(cda_ctx *ctx, const uint8_t *ods, uint32_t n_shares, uint8_t *eds, uint8_t *row_roots,
                    uint8_t *col_roots, uint8_t *data_root);
 

@@ -257,8 +257,11 @@ class PushOrderError(ValueError):
     pass
 
 
-def erasured_leaves(cells, k: int, axis_index: int):
-    """ErasuredNamespacedMerkleTree.Push for every cell of one row/column."""
+def erasured_leaves(cells, k: int, axis_index: int, blind: bool = False):
+    """ErasuredNamespacedMerkleTree.Push for every cell of one row/column.
+    blind: test/util/malicious/tree.go:18-26 BlindTree (ForceAddLeaf: no
+    namespace-order check; the malicious hasher above checks no sibling order
+    either), the tree the reference's fraud tests build unordered squares with."""
     leaves = []
     last_ns = None
     for share_index, cell in enumerate(cells):
@@ -266,7 +269,7 @@ def erasured_leaves(cells, k: int, axis_index: int):
         if len(cell) < NAMESPACE_SIZE:
             raise ValueError("data is too short to contain namespace ID")
         ns = cell[:NAMESPACE_SIZE] if (share_index < k and axis_index < k) else PARITY_NS
-        if last_ns is not None and ns < last_ns:
+        if not blind and last_ns is not None and ns < last_ns:
             raise PushOrderError(
                 "pushed data has to be lexicographically ordered by namespace IDs: "
                 f"last namespace: {last_ns.hex()}, pushed: {ns.hex()}")
@@ -275,8 +278,8 @@ def erasured_leaves(cells, k: int, axis_index: int):
     return leaves
 
 
-def axis_root(cells, k: int, axis_index: int) -> bytes:
-    return nmt_root_from_nodes(erasured_leaves(cells, k, axis_index))
+def axis_root(cells, k: int, axis_index: int, blind: bool = False) -> bytes:
+    return nmt_root_from_nodes(erasured_leaves(cells, k, axis_index, blind))
 
 
 # ---------------------------------------------------------------------------
@@ -292,11 +295,12 @@ def merkle_root(items) -> bytes:
     return sha256(NODE_PREFIX + merkle_root(items[:k]) + merkle_root(items[k:]))
 
 
-def dah_from_eds(eds: np.ndarray):
+def dah_from_eds(eds: np.ndarray, blind: bool = False):
+    """NewDataAvailabilityHeader; blind: over malicious.NewConstructor's trees."""
     W = eds.shape[0]
     k = W // 2
-    rows = [axis_root(eds[i], k, i) for i in range(W)]
-    cols = [axis_root(eds[:, j], k, j) for j in range(W)]
+    rows = [axis_root(eds[i], k, i, blind) for i in range(W)]
+    cols = [axis_root(eds[:, j], k, j, blind) for j in range(W)]
     return rows, cols, merkle_root(rows + cols)
 
 
