@@ -105,3 +105,39 @@ def test_prepare_then_process(ctx):
     bd = app.prepare_proposal_da(big, ctx=ctx)
     assert bd.square_size == 128 and 0 < len(bd.txs) < len(big)
     assert app.process_proposal_da(bd.txs, 128, bd.hash, ctx=ctx).accept
+
+
+@pytest.mark.gpu
+def test_process_proposal_mutations(ctx):
+    """TestProcessProposal's cases a DA check decides (app/test/process_proposal_test.go:92-333):
+    PrepareProposal's block data is mutated, then ProcessProposal judges it
+    against the header DataHash.  (Signature, nonce and decoding cases need
+    the ante handler and state: out of scope.)"""
+    txs = blobfactory.random_block(31, 2, 4, (1, 2), (100, 5000))     # [normal, normal, blob txs...]
+    bd = app.prepare_proposal_da(txs, ctx=ctx)
+    assert bd.txs == txs
+
+    def judge(t, size=None, h=None):
+        return app.process_proposal_da(t, bd.square_size if size is None else size, bd.hash if h is None else h,
+                                       ctx=ctx)
+
+    assert judge(bd.txs).accept                                               # valid untouched data
+    data_root_reason = "proposed data root " + bd.hash.hex().upper() + " differs from calculated data root"
+    for name, mutated in [("removed first blob tx", bd.txs[:2] + bd.txs[3:]),
+                          ("added an extra blob tx", bd.txs + [bd.txs[3]]),
+                          ("swap blobTxs", bd.txs[:2] + [bd.txs[3], bd.txs[4], bd.txs[2]] + bd.txs[5:])]:
+        v = judge(mutated)   # the reference expects REJECT; which check fires depends on the square it gives
+        assert not v.accept and (v.reason.startswith(data_root_reason) or
+                                 v.reason == "proposed square size differs from calculated square size"), name
+    # incorrectly sorted; a normal tx after a PFB: square.Construct rejects the order
+    v = judge(bd.txs[:1] + [bd.txs[2], bd.txs[1]] + bd.txs[3:])
+    assert not v.accept and v.reason.startswith("failure to compute data square from transactions: normal transaction")
+    # tampered sequence start: the header commits to share 1 with its
+    # sequence-start bit flipped (shares.Builder.FlipSequenceStart), which the
+    # honest square does not have
+    sq = list(gsq.construct(bd.txs, ctx=ctx))
+    sq[1] = sq[1][:29] + bytes([sq[1][29] ^ 1]) + sq[1][30:]
+    tampered = da.new_data_availability_header(da.extend_shares(sq)).hash()
+    assert tampered != bd.hash
+    v = judge(bd.txs, h=tampered)
+    assert not v.accept and v.reason.startswith("proposed data root " + tampered.hex().upper())
