@@ -15,7 +15,12 @@ References:
     NewDataAvailabilityHeader; the block data carries the kept txs, the
     square size and the data root;
   * pkg/appconsts/versioned_consts.go:20-27 -- both versioned constants are
-    v1's for every app version.
+    v1's for every app version;
+  * app/square_size.go:9-23 -- MaxEffectiveSquareSize: min(the blob module's
+    GovMaxSquareSize param, SquareSizeUpperBound), DefaultGovMaxSquareSize
+    (64, pkg/appconsts/initial_consts.go:10) at heights <= 1.  The proposal
+    entry points take the governance value as `gov_max_square_size` (None:
+    the hard bound, 128).
 
 Each block is one GPU submission (cda_construct_extend_dah: txs -> square ->
 EDS -> roots -> data root); for many blocks, celestia_da.replay batches the
@@ -41,6 +46,18 @@ def square_size_upper_bound(app_version: int = LATEST_VERSION) -> int:
 def subtree_root_threshold(app_version: int = LATEST_VERSION) -> int:
     """appconsts.SubtreeRootThreshold (versioned_consts.go:20-22): v1's for every version."""
     return square.SUBTREE_ROOT_THRESHOLD
+
+
+DEFAULT_GOV_MAX_SQUARE_SIZE = 64   # pkg/appconsts/initial_consts.go:10
+
+
+def max_effective_square_size(gov_max_square_size: int | None = None, app_version: int = LATEST_VERSION,
+                              height: int | None = None) -> int:
+    """App.MaxEffectiveSquareSize (app/square_size.go:9-23)."""
+    if height is not None and height <= 1:
+        return DEFAULT_GOV_MAX_SQUARE_SIZE
+    hard = square_size_upper_bound(app_version)
+    return hard if gov_max_square_size is None else min(gov_max_square_size, hard)
 
 
 def is_empty_block(txs, app_version: int = LATEST_VERSION) -> bool:
@@ -75,11 +92,12 @@ class BlockData:
     hash: bytes
 
 
-def prepare_proposal_da(txs, app_version: int = LATEST_VERSION, ctx=None) -> BlockData:
+def prepare_proposal_da(txs, app_version: int = LATEST_VERSION, ctx=None,
+                        gov_max_square_size: int | None = None) -> BlockData:
     """PrepareProposal's DA steps (:48-89) on already filtered txs: Build
     (prioritised: normal txs, then blob txs, what fits), extend, DAH hash --
     one device submission.  The reference panics where this raises."""
-    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    ub, thr = max_effective_square_size(gov_max_square_size, app_version), subtree_root_threshold(app_version)
     k, _, _, _, root, kept = square.construct_extend_dah(txs, ub, thr, build_mode=True, ctx=ctx)
     return BlockData([txs[i] for i in kept], k, root)
 
@@ -98,10 +116,10 @@ def _reason_square(err) -> str:
 
 
 def process_proposal_da(txs, square_size: int, data_hash: bytes, app_version: int = LATEST_VERSION,
-                        ctx=None) -> ProposalVerdict:
+                        ctx=None, gov_max_square_size: int | None = None) -> ProposalVerdict:
     """The data-availability checks of ProcessProposal (:122-152) for one
     block: txs, the proposer's BlockData.SquareSize and Header.DataHash."""
-    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    ub, thr = max_effective_square_size(gov_max_square_size, app_version), subtree_root_threshold(app_version)
     try:
         k, _, _, _, root, _ = square.construct_extend_dah(txs, ub, thr, ctx=ctx)
     except _lib.SquareError as e:
@@ -128,11 +146,11 @@ def _verdict(k: int, root: bytes, square_size: int, data_hash: bytes) -> Proposa
 
 
 def process_proposals_da(blocks, square_sizes, data_hashes, app_version: int = LATEST_VERSION, ctx=None,
-                         device=None) -> list[ProposalVerdict]:
+                         device=None, gov_max_square_size: int | None = None) -> list[ProposalVerdict]:
     """process_proposal_da over many blocks, the squares of one size extended
     as one device batch (celestia_da.replay)."""
     from . import replay
-    ub, thr = square_size_upper_bound(app_version), subtree_root_threshold(app_version)
+    ub, thr = max_effective_square_size(gov_max_square_size, app_version), subtree_root_threshold(app_version)
     out = []
     for r, ss, h in zip(replay.replay(blocks, None, ub, thr, ctx=ctx, device=device), square_sizes, data_hashes):
         if r.error is not None:

@@ -141,3 +141,41 @@ def test_process_proposal_mutations(ctx):
     assert tampered != bd.hash
     v = judge(bd.txs, h=tampered)
     assert not v.accept and v.reason.startswith("proposed data root " + tampered.hex().upper())
+
+
+def test_max_effective_square_size():
+    """App.MaxEffectiveSquareSize (app/square_size.go:9-23)."""
+    assert app.max_effective_square_size() == 128
+    assert app.max_effective_square_size(64) == 64
+    assert app.max_effective_square_size(256) == 128
+    assert app.max_effective_square_size(128, height=1) == app.DEFAULT_GOV_MAX_SQUARE_SIZE == 64
+
+
+# TestPrepareProposalConsistency's tx shapes (app/test/fuzz_abci_test.go:40-50):
+# (name, blob txs, blobs per tx, blob bytes), scaled where the reference's
+# count would only be dropped by Build anyway, plus its send txs (:98-108)
+CONSISTENCY_SHAPES = [
+    ("many small single share single blob transactions", 1000, 1, 400),
+    ("one hundred normal sized single blob transactions", 100, 1, 400000),
+    ("many single share multi-blob transactions", 200, 100, 400),
+    ("one hundred normal sized multi-blob transactions", 30, 4, 400000),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gov_max", [64, 128])
+def test_prepare_proposal_consistency(ctx, gov_max):
+    """Every block PrepareProposal builds is accepted by ProcessProposal
+    (fuzz_abci_test.go:26-137), for the default governance square size (64)
+    and the hard maximum, one at a time and as one replay batch."""
+    prepared = []
+    for i, (name, n, per_tx, size) in enumerate(CONSISTENCY_SHAPES):
+        txs = blobfactory.random_block(100 + i, 100, n, (per_tx, per_tx), (size, size))
+        bd = app.prepare_proposal_da(txs, ctx=ctx, gov_max_square_size=gov_max)
+        assert 1 <= bd.square_size <= gov_max and bd.txs, name
+        v = app.process_proposal_da(bd.txs, bd.square_size, bd.hash, ctx=ctx, gov_max_square_size=gov_max)
+        assert v.accept, (name, v.reason)
+        prepared.append(bd)
+    got = app.process_proposals_da([b.txs for b in prepared], [b.square_size for b in prepared],
+                                   [b.hash for b in prepared], ctx=ctx, gov_max_square_size=gov_max)
+    assert all(v.accept for v in got), [v.reason for v in got]
