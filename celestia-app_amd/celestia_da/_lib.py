@@ -64,7 +64,7 @@ EXPORTED = (
     "cda_square_layout", "cda_square_tx_share_range", "cda_square_construct", "cda_construct_extend_dah", "cda_square_construct_device",
     "cda_blob_commitments", "cda_blob_commitments_device",
     "cda_square_create", "cda_square_destroy", "cda_square_dah", "cda_square_share_proof",
-    "cda_square_blob_commitments", "cda_repair", "cda_repair_device", "cda_rs_decode",
+    "cda_square_blob_commitments", "cda_square_subtree_root", "cda_repair", "cda_repair_device", "cda_rs_decode",
     "cda_nmt_axis_roots", "cda_nmt_axis_root", "cda_nmt_prove_range", "cda_merkle_root",
     "cda_comm_unique_id", "cda_comm_init", "cda_comm_destroy", "cda_comm_size", "cda_comm_abort", "cda_extend_dah_split", "cda_split_rows_send",
     "cda_extend_dah_multi", "cda_split_layout", "cda_split_offsets", "cda_extend_dah_batch_ex",
@@ -178,6 +178,7 @@ def load(path: str | None = None):
         L.cda_square_share_proof.argtypes = [vp, C.c_uint32, C.c_uint32, u8p, u32p, u32p, i32p, i32p, u32p, u8p,
                                              u8p, u8p, u8p]
         L.cda_square_blob_commitments.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint32, u8p]
+        L.cda_square_subtree_root.argtypes = [vp, C.c_uint32, u8p, C.c_uint32, u8p]
         L.cda_repair.argtypes = [ctxp, u8p, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
         L.cda_repair_device.argtypes = [ctxp, vp, u8p, C.c_uint32, u8p, u8p, i32p, u32p]
         L.cda_rs_decode.argtypes = [ctxp, u8p, u8p, C.c_uint32, C.c_uint32, C.c_uint32]

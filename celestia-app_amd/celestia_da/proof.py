@@ -141,6 +141,15 @@ class ResidentSquare:
         b = out.tobytes()
         return [b[32 * i:32 * (i + 1)] for i in range(n)]
 
+    def subtree_root(self, row: int, walk) -> bytes:
+        """EDSSubTreeRootCacher.getSubTreeRoot (pkg/inclusion/nmt_caching.go:111-124):
+        the node of EDS row tree `row` reached by `walk` (False = WalkLeft,
+        True = WalkRight) from its root."""
+        w = np.array([1 if x else 0 for x in walk] or [0], dtype=np.uint8)
+        out = np.empty(90, dtype=np.uint8)
+        self.ctx.check(self.ctx.lib.cda_square_subtree_root(self.h, row, ptr(w), len(walk), ptr(out)))
+        return out.tobytes()
+
 
 TX_NAMESPACE = b"\x00" * 28 + b"\x01"            # go-square namespace.TxNamespace
 PAY_FOR_BLOB_NAMESPACE = b"\x00" * 28 + b"\x04"  # namespace.PayForBlobNamespace

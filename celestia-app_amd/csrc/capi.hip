@@ -573,6 +573,14 @@ int cda_square_blob_commitments(cda_square* sq, const uint32_t* starts, const ui
     });
 }
 
+int cda_square_subtree_root(cda_square* sq, uint32_t row, const uint8_t* walk, uint32_t walk_len, uint8_t* root) {
+    if (!sq) return CDA_ERR_INVALID;
+    return guarded(sq->ctx, [&](cda::Engine& e) -> int {
+        if (!root || (walk_len && !walk)) return e.fail(CDA_ERR_INVALID, "null buffer");
+        return e.square_subtree_root(&sq->sq, row, walk, walk_len, root);
+    });
+}
+
 int cda_repair(cda_ctx* ctx, uint8_t* eds, const uint8_t* present, uint32_t w, const uint8_t* row_roots,
                const uint8_t* col_roots, int32_t* byz_axis, uint32_t* byz_index) {
     return guarded(ctx, [&](cda::Engine& e) -> int {

@@ -261,6 +261,7 @@ class Engine {
         uint8_t* row_aunts;       // [rows][log2(4k)][32]
     };
     int square_share_proof(ResidentSquare* sq, uint32_t start, uint32_t end, ShareProofOut* out);
+    int square_subtree_root(ResidentSquare* sq, uint32_t row, const uint8_t* walk, uint32_t walk_len, uint8_t* out);
     int square_blob_commitments(ResidentSquare* sq, const uint32_t* starts, const uint32_t* lens, uint32_t n,
                                 uint32_t threshold, uint8_t* out);
 

@@ -15,7 +15,9 @@
 // A proof is then index arithmetic on the host (which nodes: nmt
 // buildRangeProof's maximal subtrees outside the range, RFC aunts bottom-up)
 // plus one gather launch and one copy back.
+#include <algorithm>
 #include <cstring>
+#include <string>
 
 #include "../../include/cda.h"
 #include "engine.h"
@@ -270,6 +272,37 @@ int Engine::square_share_proof(ResidentSquare* sq, uint32_t start, uint32_t end,
     if (o->row_roots) std::memcpy(o->row_roots, buf.data() + rt_off, (size_t)nrows * kNode);
     if (o->row_leaf_hash) std::memcpy(o->row_leaf_hash, buf.data() + lh_off, (size_t)nrows * 32);
     if (o->row_aunts) std::memcpy(o->row_aunts, buf.data() + au_off, (size_t)nrows * naunts * 32);
+    return CDA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// EDSSubTreeRootCacher.getSubTreeRoot (pkg/inclusion/nmt_caching.go:111-124,
+// walk :51-78): the node of row tree `row` reached from its root by `walk`
+// (0 = WalkLeft, 1 = WalkRight).  The cache holds inner nodes only, so a walk
+// may end on a leaf but not continue below one.
+// ---------------------------------------------------------------------------
+int Engine::square_subtree_root(ResidentSquare* sq, uint32_t row, const uint8_t* walk, uint32_t walk_len,
+                                uint8_t* out) {
+    const uint32_t W = 2 * sq->k, logW = sq->log_w;
+    if (row >= W)
+        return fail(CDA_ERR_INVALID,
+                    "row exceeds range of cache: max " + std::to_string(W) + " got " + std::to_string(row));
+    const uint32_t d = std::min(walk_len, logW);
+    uint32_t pos = 0;
+    for (uint32_t i = 0; i < d; i++) pos = 2 * pos + (walk[i] ? 1u : 0u);
+    const uint32_t L = logW - d;
+    // the levels below the root are kept per row tree; the root itself is the row root
+    const GatherPiece piece = L == logW
+                                  ? GatherPiece{GatherPiece::kRows, (uint64_t)row * kNode, 0, kNode}
+                                  : GatherPiece{GatherPiece::kLevels,
+                                                sq->level_offset(L) + ((uint64_t)row * (W >> L) + pos) * kSlot, 0, kNode};
+    int rc;
+    if ((rc = square_gather(sq, {piece}, out, kNode))) return rc;
+    if (walk_len > logW) {   // walk(leaf, rest): the leaf is not in the cache -- Go's %v of its bytes
+        std::string msg = "did not find sub tree root: [";
+        for (uint32_t i = 0; i < kNode; i++) msg += (i ? " " : "") + std::to_string(out[i]);
+        return fail(CDA_ERR_INVALID, msg + "]");
+    }
     return CDA_OK;
 }
 

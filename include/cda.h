@@ -426,6 +426,13 @@ int cda_square_share_proof(cda_square *sq, uint32_t start, uint32_t end, uint8_t
  * reference does) and spans share_lens[i] shares; commitments n*32. */
 int cda_square_blob_commitments(cda_square *sq, const uint32_t *starts, const uint32_t *share_lens, uint32_t n,
                                 uint32_t threshold, uint8_t *commitments);
+/* EDSSubTreeRootCacher.getSubTreeRoot (pkg/inclusion/nmt_caching.go:111-124):
+ * the 90-B node of row tree `row` (0 <= row < 2k) reached from its root by
+ * walk[0 .. walk_len) (0 = WalkLeft, 1 = WalkRight; GetCommitment prefixes
+ * WalkLeft for the ODS half).  A walk longer than the tree's depth fails with
+ * the cache's "did not find sub tree root: [...]" (root still receives the
+ * leaf it reached); row >= 2k: "row exceeds range of cache: max %d got %d". */
+int cda_square_subtree_root(cda_square *sq, uint32_t row, const uint8_t *walk, uint32_t walk_len, uint8_t *root);
 
 /* ---- Repair ------------------------------------------
  * rsmt2d ExtendedDataSquare.Repair(rowRoots, colRoots) (EXT v0.14.0,

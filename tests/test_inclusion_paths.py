@@ -71,3 +71,40 @@ def test_walk_cached_subtree_root():
         assert opr.walk_subtree_root(tree, walk) == want
     with pytest.raises(KeyError, match="did not find sub tree root"):
         opr.walk_subtree_root(tree, [R, R, R, R])
+
+
+# ---- TestEDSSubRootCacher (nmt_caching_test.go:117-137) on the resident square
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [8, 32])
+def test_eds_subtree_root_cacher(ctx, k):
+    """getSubTreeRoot(dah, row, [L, L, L]) of every ODS row equals the root of
+    an erasured tree over the row's first 2k >> 3 shares (the reference's
+    calculateSubTreeRoots), and every walk equals the oracle's walk on the
+    row's leaves; the cache's errors."""
+    import numpy as np
+    import pyref
+    from celestia_da import CdaError, testfactory
+    from celestia_da import proof as gpr
+    ods = testfactory.random_square(k, 9)
+    eds = pyref.extend_square(ods.reshape(k, k, 512))
+    sq = gpr.ResidentSquare(ods)
+    try:
+        L, R = opr.WALK_LEFT, opr.WALK_RIGHT
+        n = 2 * k >> 3
+        for i in range(k):
+            want = pyref.axis_root([bytes(c) for c in eds[i, :n]], n, 0)   # calculateSubTreeRoots
+            assert sq.subtree_root(i, [L, L, L]) == want
+        rng = np.random.default_rng(1)
+        depth = (2 * k).bit_length() - 1
+        for _ in range(24):
+            r = int(rng.integers(2 * k))
+            walk = [bool(b) for b in rng.integers(0, 2, int(rng.integers(0, depth + 1)))]
+            leaves = pyref.erasured_leaves([bytes(c) for c in eds[r]], k, r)
+            assert sq.subtree_root(r, walk) == opr.walk_subtree_root(leaves, walk)
+        assert sq.subtree_root(0, []) == sq.dah()[0][0]
+        with pytest.raises(CdaError, match="did not find sub tree root"):
+            sq.subtree_root(0, [L] * (depth + 1))
+        with pytest.raises(CdaError, match=f"row exceeds range of cache: max {2 * k} got {2 * k}"):
+            sq.subtree_root(2 * k, [L])
+    finally:
+        sq.close()
