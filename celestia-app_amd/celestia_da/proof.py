@@ -151,6 +151,32 @@ class ResidentSquare:
         return out.tobytes()
 
 
+def _go_namespace(ns: bytes) -> str:
+    """fmt %v of a go-square namespace.Namespace{Version, ID}."""
+    return "{%d [%s]}" % (ns[0], " ".join(str(b) for b in ns[1:]))
+
+
+def parse_namespace(raw_shares, start_share: int, end_share: int) -> bytes:
+    """proof.ParseNamespace (pkg/proof/querier.go:134-166): the one namespace
+    (29 bytes) of shares [start_share, end_share), with the reference's
+    error texts (ValueError)."""
+    if start_share < 0:
+        raise ValueError(f"start share {start_share} should be positive")
+    if end_share < 0:
+        raise ValueError(f"end share {end_share} should be positive")
+    if end_share <= start_share:
+        raise ValueError(f"end share {end_share} cannot be lower or equal to the starting share {start_share}")
+    if end_share > len(raw_shares):
+        raise ValueError(f"end share {end_share} is higher than block shares {len(raw_shares)}")
+    first = bytes(raw_shares[start_share][:29])
+    for i, sh in enumerate(raw_shares[start_share:end_share]):
+        ns = bytes(sh[:29])
+        if ns != first:
+            raise ValueError(f"shares range contain different namespaces at index {i}: "
+                             f"{_go_namespace(first)} and {_go_namespace(ns)} ")
+    return first
+
+
 TX_NAMESPACE = b"\x00" * 28 + b"\x01"            # go-square namespace.TxNamespace
 PAY_FOR_BLOB_NAMESPACE = b"\x00" * 28 + b"\x04"  # namespace.PayForBlobNamespace
 

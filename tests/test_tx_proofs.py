@@ -175,3 +175,78 @@ def test_all_shares_inclusion_proof(ctx):
     bad = to_dict(p)
     bad["data"] = [bytes(512)] + bad["data"][1:]
     assert opr.share_proof_validate(bad, root) is not None
+
+
+def _share_proof_block():
+    """TestNewShareInclusionProof's block (pkg/proof/proof_test.go:98-107): 50
+    random txs of 500 B, then three blob txs with one 500-B blob each in ns1,
+    ns2, ns3 (appns.MustNewV0 of ten 0x01 / 0x02 / 0x03 bytes)."""
+    rng = np.random.default_rng(23)
+    txs = [blobfactory.normal_tx(rng, 500) for _ in range(50)]
+    for b in (1, 2, 3):   # signed PFB txs of ~450 B: three compact shares, as in the reference's square
+        inner = rng.integers(0, 256, 450, dtype=np.uint8).tobytes()
+        txs.append(blobfactory.blob_tx(inner, [(b"\x00" * 18 + bytes([b]) * 10,
+                                                 rng.integers(0, 256, 500, dtype=np.uint8).tobytes())]))
+    return txs
+
+
+NS = {b: b"\x00" * 19 + bytes([b]) * 10 for b in (1, 2, 3)}
+# (name, start, end, namespace or None when ParseNamespace must fail), proof_test.go:122-209
+SHARE_PROOF_CASES = [
+    ("negative starting share", -1, 99, None),
+    ("negative ending share", 0, -99, None),
+    ("ending share lower than starting share", 1, 0, None),
+    ("ending share is equal to the starting share", 1, 1, None),
+    ("ending share higher than number of shares available in square size of 32", 0, 4097, None),
+    ("1 transaction share", 0, 1, gpr.TX_NAMESPACE),
+    ("10 transaction shares", 0, 10, gpr.TX_NAMESPACE),
+    ("53 transaction shares", 0, 53, gpr.TX_NAMESPACE),
+    ("shares from different namespaces", 48, 55, None),
+    ("shares from PFB namespace", 53, 55, gpr.PAY_FOR_BLOB_NAMESPACE),
+    ("blob shares for first namespace", 56, 58, NS[1]),
+    ("blob shares for third namespace", 60, 62, NS[3]),
+]
+
+
+def test_parse_namespace_cases():
+    """ParseNamespace over the reference test's square shape: the same share
+    indexes hold the same namespaces (53 tx shares, the PFB shares, 2-share
+    blobs at 56 and 60), and the error cases fail with querier.go's texts."""
+    shares, k, _, _ = osq.builder(_share_proof_block(), 128, 64, "construct")
+    assert k == 8
+    for name, s, e, ns in SHARE_PROOF_CASES:
+        if ns is None:
+            with pytest.raises(ValueError):
+                gpr.parse_namespace(shares, s, e)
+        else:
+            assert gpr.parse_namespace(shares, s, e) == ns, name
+    with pytest.raises(ValueError, match="start share -1 should be positive"):
+        gpr.parse_namespace(shares, -1, 99)
+    with pytest.raises(ValueError, match="end share 0 cannot be lower or equal to the starting share 1"):
+        gpr.parse_namespace(shares, 1, 0)
+    with pytest.raises(ValueError, match="end share 4097 is higher than block shares 64"):
+        gpr.parse_namespace(shares, 0, 4097)
+    with pytest.raises(ValueError) as e:
+        gpr.parse_namespace(shares, 48, 55)
+    assert str(e.value) == ("shares range contain different namespaces at index 5: {0 [" + " ".join(["0"] * 27) +
+                            " 1]} and {0 [" + " ".join(["0"] * 27) + " 4]} ")
+
+
+@pytest.mark.gpu
+def test_new_share_inclusion_proof_cases(ctx):
+    """TestNewShareInclusionProof (proof_test.go:98-238): every range
+    ParseNamespace accepts gets a GPU proof that validates against the data
+    root."""
+    shares, k, _, _ = osq.builder(_share_proof_block(), 128, 64, "construct")
+    ods = np.frombuffer(b"".join(shares), dtype=np.uint8).reshape(-1, 512).copy()
+    _, _, _, root = oracle_eds(ods, k)
+    sq = gpr.ResidentSquare(ods)
+    try:
+        for name, s, e, ns in SHARE_PROOF_CASES:
+            if ns is None:
+                continue
+            p = sq.share_proof(gpr.parse_namespace(shares, s, e), s, e)
+            assert opr.share_proof_validate(to_dict(p), root) is None, name
+            assert p.data == shares[s:e]
+    finally:
+        sq.close()
