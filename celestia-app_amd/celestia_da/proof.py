@@ -215,9 +215,30 @@ def new_tx_inclusion_proof(txs, tx_index: int, app_version: int = 2, ctx=None) -
     """NewTxInclusionProof (proof.go:22-49): the share proof of the shares that
     hold tx tx_index of the block, in the square square.Construct builds."""
     from . import square
+    if tx_index < 0:   # the Go parameter is a uint64
+        raise _lib.CdaError(_lib.CDA_ERR_INVALID, f"txIndex {tx_index} is negative")
     if tx_index >= len(txs):
         raise _lib.CdaError(_lib.CDA_ERR_INVALID, f"txIndex {tx_index} out of bounds")
     ub, thr = square.SQUARE_SIZE_UPPER_BOUND, square.SUBTREE_ROOT_THRESHOLD   # appconsts, every version
     start, end, ns = tx_share_range(txs, tx_index, ub, thr)
     sq = square.construct(txs, ub, thr, ctx=ctx)
     return new_share_inclusion_proof(sq.to_bytes(), ns, start, end, ctx)
+
+
+def query_tx_inclusion_proof(path, txs, app_version: int = 2, ctx=None) -> ShareProof:
+    """QueryTxInclusionProof's index handling (pkg/proof/querier.go:29-57) over
+    a block's txs (the ABCI query's protobuf block is the caller's): path is
+    the query path, [index]; errors are ValueError with the reference texts."""
+    if len(path) != 1:
+        raise ValueError(f"expected query path length: 1 actual: {len(path)} ")
+    try:
+        if not path[0] or path[0].strip() != path[0]:
+            raise ValueError
+        index = int(path[0], 10)
+    except ValueError:
+        raise ValueError(f'strconv.ParseInt: parsing "{path[0]}": invalid syntax') from None
+    if not -(1 << 63) <= index < (1 << 63):
+        raise ValueError(f'strconv.ParseInt: parsing "{path[0]}": value out of range')
+    if index < 0:
+        raise ValueError(f'path[0] element: "{path[0]}" produced a negative value: {index}')
+    return new_tx_inclusion_proof(txs, index, app_version, ctx)

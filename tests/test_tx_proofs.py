@@ -250,3 +250,19 @@ def test_new_share_inclusion_proof_cases(ctx):
             assert p.data == shares[s:e]
     finally:
         sq.close()
+
+
+def test_query_tx_inclusion_proof_rejects_negative_values():
+    """TestQueryTxInclusionProofRejectsNegativeValues (proof_test.go:270-287)
+    and the querier's other index checks (querier.go:29-40)."""
+    with pytest.raises(ValueError, match="negative") as e:
+        gpr.query_tx_inclusion_proof(["-2"], [])
+    assert str(e.value) == 'path[0] element: "-2" produced a negative value: -2'
+    with pytest.raises(ValueError, match="expected query path length: 1 actual: 2 "):
+        gpr.query_tx_inclusion_proof(["1", "2"], [])
+    with pytest.raises(ValueError, match='parsing "x1": invalid syntax'):
+        gpr.query_tx_inclusion_proof(["x1"], [])
+    with pytest.raises(ValueError, match="value out of range"):
+        gpr.query_tx_inclusion_proof([str(1 << 63)], [])
+    with pytest.raises(CdaError, match="txIndex -1 is negative"):
+        gpr.new_tx_inclusion_proof([b"x"], -1)
