@@ -232,7 +232,7 @@ def query_tx_inclusion_proof(path, txs, app_version: int = 2, ctx=None) -> Share
     if len(path) != 1:
         raise ValueError(f"expected query path length: 1 actual: {len(path)} ")
     try:
-        if not path[0] or path[0].strip() != path[0]:
+        if not path[0] or path[0].strip() != path[0] or "_" in path[0]:   # Go's base-10 syntax
             raise ValueError
         index = int(path[0], 10)
     except ValueError:
