@@ -12,7 +12,15 @@
  *      text "number of shares is not a power of 2: got 5" (:68);
  *   3. cda_dah_from_eds on an EDS whose Q0 row 0 is out of namespace order:
  *      CDA_ERR_PUSH_ORDER, the nmt message, and cda_push_order_detail =
- *      (row axis, row 0, position 1).
+ *      (row axis, row 0, position 1);
+ *   4. a resident square (cda_square_create, the proof / GetCommitment
+ *      cache): its DAH equals the golden k = 2 root, the subtree root of the
+ *      empty walk is row root 0, the walk [WalkLeft] is the standalone
+ *      erasured tree over row 0's two ODS cells (cda_nmt_axis_root), a walk
+ *      below the leaves fails with the cache's text;
+ *   5. rsmt2d Codec.Encode / Decode (cda_rs_encode / cda_rs_decode): 8 data
+ *      shards, half of data + parity erased, reconstructed bit-exactly;
+ *   6. Repair (cda_repair) of the k = 2 EDS with Q0 erased: the EDS back.
  * Prints "c host ok" and exits 0, or names the failed check and exits 1.
  * Build: gcc -std=c11 -I include tests/c_host/cda_host_smoke.c
  *        -L celestia-app_amd -lcda -Wl,-rpath,<abs celestia-app_amd>
@@ -107,6 +115,63 @@ int main(void) {
     cda_push_order_detail(ctx, &axis, &index, &position);
     if (axis != 0 || index != 0 || position != 1) return fail("push-order detail");
     (void)k;
+
+    /* 4. resident square of the k = 2 constant shares */
+    {
+        uint8_t ods2[4 * 512], r0[90], sub[90], want[90], dr[32], rr[4 * 90];
+        char got[65];
+        uint32_t kk = 0;
+        cda_square* sq = NULL;
+        constant_shares(ods2, 4);
+        if (cda_square_create(ctx, ods2, 4, &sq) != CDA_OK) return fail("cda_square_create");
+        if (cda_square_dah(sq, &kk, rr, NULL, dr, NULL) != CDA_OK || kk != 2) return fail("cda_square_dah");
+        hex(dr, 32, got);
+        if (strcmp(got, golden_k2)) return fail("resident square data root");
+        if (cda_square_subtree_root(sq, 0, NULL, 0, r0) != CDA_OK || memcmp(r0, rr, 90))
+            return fail("subtree root of the empty walk");
+        const uint8_t left[1] = {0};
+        if (cda_square_subtree_root(sq, 0, left, 1, sub) != CDA_OK) return fail("subtree root [WalkLeft]");
+        if (cda_nmt_axis_root(ctx, ods2, 512, 2, 2, 0, want) != CDA_OK || memcmp(sub, want, 90))
+            return fail("subtree root [WalkLeft] vs the standalone tree");
+        const uint8_t deep[3] = {0, 0, 0};
+        if (cda_square_subtree_root(sq, 0, deep, 3, sub) != CDA_ERR_INVALID ||
+            !strstr(cda_last_error(ctx), "did not find sub tree root"))
+            return fail("walk below the leaves");
+        cda_square_destroy(sq);
+    }
+
+    /* 5. Codec.Encode / Decode: 8 data shards of 64 B, half of the 16 lost */
+    {
+        uint8_t shards[16 * 64], keep[16 * 64], present[16];
+        for (int i = 0; i < 8 * 64; i++) shards[i] = (uint8_t)(i * 37 + 11);
+        if (cda_rs_encode(ctx, shards, 8, 64, 1, shards + 8 * 64) != CDA_OK) return fail("cda_rs_encode");
+        memcpy(keep, shards, sizeof keep);
+        for (int i = 0; i < 16; i++) {
+            present[i] = (i % 2 == 0);
+            if (!present[i]) memset(shards + i * 64, 0xA5, 64);
+        }
+        if (cda_rs_decode(ctx, shards, present, 8, 64, 1) != CDA_OK) return fail("cda_rs_decode");
+        if (memcmp(shards, keep, sizeof keep)) return fail("decoded shards");
+        memset(present, 0, 9);   /* 7 of 16 left */
+        if (cda_rs_decode(ctx, shards, present, 8, 64, 1) != CDA_ERR_UNREPAIRABLE) return fail("too few shards");
+    }
+
+    /* 6. Repair of the k = 2 EDS with Q0 erased */
+    {
+        uint8_t ods2[4 * 512], eds2[16 * 512], keep[16 * 512], rr[4 * 90], cr[4 * 90], dr[32], present[16];
+        int32_t byz_axis = -1;
+        uint32_t byz_index = 0;
+        constant_shares(ods2, 4);
+        ods2[29] = 0x07;   /* not all cells equal */
+        if (cda_extend_dah(ctx, ods2, 4, eds2, rr, cr, dr) != CDA_OK) return fail("extend for repair");
+        memcpy(keep, eds2, sizeof keep);
+        for (int i = 0; i < 16; i++) {
+            present[i] = !((i / 4) < 2 && (i % 4) < 2);
+            if (!present[i]) memset(eds2 + i * 512, 0, 512);
+        }
+        if (cda_repair(ctx, eds2, present, 4, rr, cr, &byz_axis, &byz_index) != CDA_OK) return fail("cda_repair");
+        if (memcmp(eds2, keep, sizeof keep)) return fail("repaired EDS");
+    }
 
     cda_ctx_destroy(ctx);
     printf("c host ok: %s\n", cda_version());
