@@ -225,20 +225,40 @@ def new_tx_inclusion_proof(txs, tx_index: int, app_version: int = 2, ctx=None) -
     return new_share_inclusion_proof(sq.to_bytes(), ns, start, end, ctx)
 
 
+def _parse_int64(text: str) -> int:
+    """strconv.ParseInt(text, 10, 64) with Go's error texts (ValueError)."""
+    if not text or text.strip() != text or "_" in text:   # Go's base-10 syntax
+        raise ValueError(f'strconv.ParseInt: parsing "{text}": invalid syntax')
+    try:
+        v = int(text, 10)
+    except ValueError:
+        raise ValueError(f'strconv.ParseInt: parsing "{text}": invalid syntax') from None
+    if not -(1 << 63) <= v < (1 << 63):
+        raise ValueError(f'strconv.ParseInt: parsing "{text}": value out of range')
+    return v
+
+
 def query_tx_inclusion_proof(path, txs, app_version: int = 2, ctx=None) -> ShareProof:
     """QueryTxInclusionProof's index handling (pkg/proof/querier.go:29-57) over
     a block's txs (the ABCI query's protobuf block is the caller's): path is
     the query path, [index]; errors are ValueError with the reference texts."""
     if len(path) != 1:
         raise ValueError(f"expected query path length: 1 actual: {len(path)} ")
-    try:
-        if not path[0] or path[0].strip() != path[0] or "_" in path[0]:   # Go's base-10 syntax
-            raise ValueError
-        index = int(path[0], 10)
-    except ValueError:
-        raise ValueError(f'strconv.ParseInt: parsing "{path[0]}": invalid syntax') from None
-    if not -(1 << 63) <= index < (1 << 63):
-        raise ValueError(f'strconv.ParseInt: parsing "{path[0]}": value out of range')
+    index = _parse_int64(path[0])
     if index < 0:
         raise ValueError(f'path[0] element: "{path[0]}" produced a negative value: {index}')
     return new_tx_inclusion_proof(txs, index, app_version, ctx)
+
+
+def query_share_inclusion_proof(path, txs, app_version: int = 2, ctx=None) -> ShareProof:
+    """QueryShareInclusionProof (pkg/proof/querier.go:72-128): path = [begin,
+    end]; the block's square is square.Construct at the version's upper bound,
+    the range must hold one namespace (ParseNamespace), then
+    NewShareInclusionProof on the GPU."""
+    from . import square
+    if len(path) != 2:
+        raise ValueError(f"expected query path length: 2 actual: {len(path)} ")
+    begin, end = _parse_int64(path[0]), _parse_int64(path[1])
+    sq = square.construct(txs, square.SQUARE_SIZE_UPPER_BOUND, square.SUBTREE_ROOT_THRESHOLD, ctx=ctx)
+    ns = parse_namespace(sq, begin, end)
+    return new_share_inclusion_proof(sq.to_bytes(), ns, begin, end, ctx)

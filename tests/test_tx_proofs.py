@@ -266,3 +266,29 @@ def test_query_tx_inclusion_proof_rejects_negative_values():
         gpr.query_tx_inclusion_proof([str(1 << 63)], [])
     with pytest.raises(CdaError, match="txIndex -1 is negative"):
         gpr.new_tx_inclusion_proof([b"x"], -1)
+
+
+def test_query_share_inclusion_proof_path_errors():
+    """QueryShareInclusionProof's path checks (querier.go:72-84) and the
+    ParseNamespace texts it passes through."""
+    with pytest.raises(ValueError, match="expected query path length: 2 actual: 1 "):
+        gpr.query_share_inclusion_proof(["3"], [])
+    with pytest.raises(ValueError, match='parsing "a": invalid syntax'):
+        gpr.query_share_inclusion_proof(["a", "5"], [])
+
+
+@pytest.mark.gpu
+def test_query_share_inclusion_proof(ctx):
+    """custom/shareInclusionProof/56/58 over the block of
+    TestNewShareInclusionProof: ns1's blob shares, validated."""
+    txs = _share_proof_block()
+    shares, k, _, _ = osq.builder(txs, 128, 64, "construct")
+    ods = np.frombuffer(b"".join(shares), dtype=np.uint8).reshape(-1, 512).copy()
+    _, _, _, root = oracle_eds(ods, k)
+    p = gpr.query_share_inclusion_proof(["56", "58"], txs)
+    assert bytes([p.namespace_version]) + p.namespace_id == NS[1]
+    assert opr.share_proof_validate(to_dict(p), root) is None
+    with pytest.raises(ValueError, match="shares range contain different namespaces"):
+        gpr.query_share_inclusion_proof(["48", "55"], txs)
+    with pytest.raises(ValueError, match="start share -1 should be positive"):   # after Construct, as in Go
+        gpr.query_share_inclusion_proof(["-1", "5"], txs)
