@@ -126,3 +126,27 @@ def test_get_commitment_gpu(ctx, seed, max_ss):
             sq.blob_commitments([k * k - 1], [2])
     finally:
         sq.close()
+
+
+@pytest.mark.gpu
+def test_resident_square_k1(ctx):
+    """The smallest square (MinDataAvailabilityHeader's tail-padding share,
+    data_availability_header_test.go:27-32) through every resident-square
+    entry point: the golden data root, the one-share proof, the walks of a
+    two-leaf row tree, a one-share commitment."""
+    from celestia_da import da
+    from test_share_proof_validate import to_dict
+    share = da.tail_padding_share()
+    sq = gpr.ResidentSquare(np.frombuffer(share, dtype=np.uint8).copy())
+    try:
+        rows, cols, root = sq.dah()
+        assert root.hex() == "3d96b7d238e7e0456f6af8e7cdf0a67bd6cf9c2089ecb559c659dcaa1f880353"
+        p = sq.share_proof(share[:29], 0, 1)
+        assert opr.share_proof_validate(to_dict(p), root) is None and p.data == [share]
+        leaves = pyref.erasured_leaves([share, bytes(sq.eds()[0][1])], 1, 0)
+        assert sq.subtree_root(0, []) == rows[0]
+        assert sq.subtree_root(0, [False]) == leaves[0] and sq.subtree_root(1, [True]) == pyref.erasured_leaves(
+            [bytes(c) for c in sq.eds()[1]], 1, 1)[1]
+        assert sq.blob_commitments([0], [1]) == [opr.get_commitment(sq.eds(), 1, 0, 1)]
+    finally:
+        sq.close()
