@@ -150,3 +150,38 @@ def test_resident_square_k1(ctx):
         assert sq.blob_commitments([0], [1]) == [opr.get_commitment(sq.eds(), 1, 0, 1)]
     finally:
         sq.close()
+
+
+@pytest.mark.gpu
+def test_resident_square_k512():
+    """The largest square this library extends (config 3, GF(2^16)) as a
+    resident square: its data root equals tests/golden/k512.json's, and share
+    proofs across the square validate against it (the proof nodes and aunts come from every cached level); a
+    subtree walk of row 1 023 (a Q2 | Q3 row) equals the tree
+    over that row's cells."""
+    import json
+    import os
+    from celestia_da import testfactory
+    from test_share_proof_validate import to_dict
+    k = 512
+    want = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "k512.json")))["squares"]["0"]
+    ods = testfactory.random_square(k, 0)
+    sq = gpr.ResidentSquare(ods)
+    try:
+        rows, _, root = sq.dah()
+        assert root.hex() == want["data_root"]
+        shares = ods.reshape(-1, 512)
+        # every share of a random square has its own namespace, so the proofs
+        # are of single shares (Validate needs one namespace): first / last of
+        # rows, the middle, the last ODS share
+        for s in (0, 5, k - 1, k, 3 * k + 100, k * k // 2 + 17, k * k - 1):
+            p = sq.share_proof(bytes(shares[s][:29]), s, s + 1)
+            assert opr.share_proof_validate(to_dict(p), root) is None, s
+            assert p.data == [bytes(shares[s])]
+        eds_row = sq.eds()[2 * k - 1]
+        leaves = pyref.erasured_leaves([bytes(c) for c in eds_row], k, 2 * k - 1)
+        walk = [True, False, True, True, False, False, True, False, True]
+        assert sq.subtree_root(2 * k - 1, walk) == opr.walk_subtree_root(leaves, walk)
+        assert sq.subtree_root(2 * k - 1, []) == rows[2 * k - 1]
+    finally:
+        sq.close()
