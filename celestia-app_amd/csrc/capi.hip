@@ -24,12 +24,14 @@ struct cda_square {
 
 namespace {
 
-// pkg/da/data_availability_header.go SquareSize + IsPowerOfTwo
+// pkg/da/data_availability_header.go SquareSize + IsPowerOfTwo; a power of
+// two that is not a square (8 shares) passes ExtendShares' check and fails in
+// rsmt2d's newDataSquare instead
 bool square_width(uint32_t n_shares, uint32_t* k) {
     if (n_shares == 0 || (n_shares & (n_shares - 1))) return false;
     uint32_t w = 1;
     while ((uint64_t)w * w < n_shares) w <<= 1;
-    if ((uint64_t)w * w != n_shares) return false;   // e.g. 8 shares: power of two, not a square
+    if ((uint64_t)w * w != n_shares) return false;
     *k = w;
     return true;
 }
@@ -114,7 +116,11 @@ int guarded_stream(cda_ctx* ctx, void* stream, F&& f) {
     return guarded_on(ctx, &s, [&](cda::Engine& e) { return f(e, s); });
 }
 
+// The error of a share count square_width rejects: ExtendShares' own
+// (data_availability_header.go:67-69), or rsmt2d's for a power of two that is
+// not a square (newDataSquare, EXT v0.14.0).
 int not_pow2(cda::Engine& e, uint32_t n) {
+    if (n && !(n & (n - 1))) return e.fail(CDA_ERR_INVALID, "number of chunks must be a square number");
     char buf[96];
     snprintf(buf, sizeof buf, "number of shares is not a power of 2: got %u", n);
     return e.fail(CDA_ERR_NOT_POW2, buf);

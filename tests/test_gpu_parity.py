@@ -93,6 +93,17 @@ def test_extend_shares_errors(ctx):
         da.extend_shares(pyref.constant_shares(129 * 129))
     with pytest.raises(ValueError, match="not a power of 2"):
         da.extend_shares(pyref.constant_shares(5))
+    # a power of two that is not a square passes ExtendShares' check and fails
+    # in rsmt2d's newDataSquare -- in the Python mirror and in the C ABI
+    with pytest.raises(ValueError, match="number of chunks must be a square number"):
+        da.extend_shares(pyref.constant_shares(8))
+    from celestia_da._lib import CDA_ERR_INVALID, CDA_ERR_NOT_POW2, ptr
+    eds = np.empty(16 * 512, dtype=np.uint8)
+    for n, code, text in [(8, CDA_ERR_INVALID, "number of chunks must be a square number"),
+                          (5, CDA_ERR_NOT_POW2, "number of shares is not a power of 2: got 5")]:
+        ods = np.frombuffer(b"".join(pyref.constant_shares(n)), dtype=np.uint8).copy()
+        assert ctx.lib.cda_extend_shares(ctx.h, ptr(ods), n, ptr(eds)) == code
+        assert ctx.lib.cda_last_error(ctx.h).decode() == text
 
 
 def test_push_order_error(ctx):
