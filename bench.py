@@ -989,15 +989,27 @@ def main():
     if mode == "spawn":   # before torch is imported: the parent never touches the GPU
         sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg5 = None
+    if (world > 1 or args.config5) and not args.no_extras and not args.config5_child:
+        # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
+        # all-to-all of the row-encoded blocks, column encode + hashing per
+        # rank, gather of subtree/column roots, combine on rank 0), run by a
+        # child process per rank with its own process group: a collective that
+        # never returns or a crash there must not cost the headline line.  It
+        # runs FIRST, before this rank touches the GPU, so a rank and its child
+        # never hold the GPU together: N ranks + N children + a launcher agent
+        # would pass a box's 16-processes-per-GPU cap at N = 8
+        # (profiles/r06/gpu_procs.txt).
+        cfg5 = config5_isolated(world, CONFIG5_TIMEOUT_S)
+
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from celestia_da import Context, testfactory
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (never set by the driver): CDA_BENCH_DEVICE puts every
     # rank on one device and CDA_BENCH_BACKEND=gloo replaces RCCL for the
     # parent group, so the N > 1 flow runs on a one-GPU box
@@ -1363,15 +1375,8 @@ def main():
             "extras": extras,
         }
 
-    if (world > 1 or args.config5) and not args.no_extras:
-        # config 5: ONE k=512 square split by row blocks over all ranks (RCCL
-        # all-to-all of the row-encoded blocks, column encode + hashing per
-        # rank, gather of subtree/column roots, combine on rank 0), run by a
-        # child process per rank with its own process group: a collective that
-        # never returns or a crash there must not cost the headline line.
-        if dist.is_initialized():
-            dist.barrier()   # rank 0 ran the extras meanwhile: start the children together
-        extras["config5"] = config5_isolated(world, CONFIG5_TIMEOUT_S)
+    if cfg5 is not None:   # measured first, see above
+        extras["config5"] = cfg5
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
